@@ -1,0 +1,251 @@
+"""Headline benchmark: Llama-3-8B NF4 (double quant) batch-1 greedy decode on MI355X
+(BASELINE.json configs[1]) plus the 4096x4096 decode-GEMV roofline and the
+config #1 CPU dequant+matmul baseline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+* Model: transformers LlamaForCausalLM with the Llama-3-8B architecture,
+  random-init fp16 weights (no network -> no checkpoint), every decoder
+  nn.Linear replaced by quantizations_amd.Linear4bit(quant_type="nf4",
+  compress_statistics=True) through replace_with_bnb_linear; lm_head stays
+  fp16 (transformers' default skip list).  A step = one generated token
+  (full forward: embeddings, 32 layers with attention + KV cache, lm_head,
+  argmax).  value = generated tokens / s.
+* N > 1 (torchrun, one process per GPU): every Linear4bit is row-sharded
+  (rows p*M/N..(p+1)*M/N on rank p, sliced from the global quant state) and
+  its output all-gathered over RCCL; the same single decode stream is served
+  by all N GPUs (strong scaling).
+* roofline: the 4096x4096 NF4+DQ fused GEMV alone, 64 rotating weight copies
+  (> the 256 MiB Infinity Cache), per-launch HIP events on the launch stream;
+  algorithmic bytes per launch = 8,672,324.
+* cpu_baseline (rank 0, N = 1): the oracle's CPU dequant + torch.matmul of one
+  Linear4bit(4096,4096) NF4 layer (config #1), scaled to the 224 Linear4bit
+  layers of one token.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                 num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
+                 rms_norm_eps=1e-5, tie_word_embeddings=False)
+# Linear4bit shapes of one Llama-3-8B layer (q, k, v, o, gate, up, down) as (M, K)
+LAYER_SHAPES = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
+GEMV_BYTES_4096 = 8_672_324  # packed 8,388,608 + qabsmax 262,144 + absmax2 4,096 + offset 4 + code2 1,024 + LUT 64
+#                              + x 8,192 + y 8,192   
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(layers: int, seed: int):
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import replace_with_bnb_linear
+
+    cfg = LlamaConfig(**{**LLAMA3_8B, "num_hidden_layers": layers})
+    torch.manual_seed(seed)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float16)
+    with torch.device("cuda"):
+        model = LlamaForCausalLM(cfg)
+    torch.set_default_dtype(prev)
+    model.eval()
+    replace_with_bnb_linear(model, modules_to_not_convert=["lm_head"], quant_type="nf4", compress_statistics=True,
+                            compute_dtype=torch.float32)
+    torch.cuda.empty_cache()
+    return model, cfg
+
+
+@torch.inference_mode()
+def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: int):
+    from transformers.cache_utils import DynamicCache
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    ids = torch.randint(0, cfg.vocab_size, (1, prompt_len), generator=g).to(dev)
+    cache = DynamicCache()
+    out = model(input_ids=ids, past_key_values=cache, use_cache=True)      # prefill (fused MFMA GEMM path)
+    nxt = out.logits[:, -1:].argmax(-1)
+    for _ in range(warmup):
+        out = model(input_ids=nxt, past_key_values=cache, use_cache=True)
+        nxt = out.logits[:, -1:].argmax(-1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    toks = []
+    for _ in range(steps):
+        out = model(input_ids=nxt, past_key_values=cache, use_cache=True)
+        nxt = out.logits[:, -1:].argmax(-1)
+        toks.append(nxt)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    return dt, torch.cat(toks, dim=1)
+
+
+@torch.inference_mode()
+def gemv_roofline(copies: int = 64, iters: int = 400):
+    """Per-launch duration of the 4096x4096 NF4+DQ fused GEMV (rotating weights)."""
+    from quantizations_amd import _lib
+    from quantizations_amd.core import quantize_4bit
+
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    W = (torch.randn(4096, 4096, device=dev) * 0.02).to(torch.float16)
+    packed, qs = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    sets = [(packed.clone(), qs.absmax.clone(), qs.state2.absmax.clone()) for _ in range(copies)]
+    x = torch.randn(4096, device=dev).to(torch.float16)
+    y = torch.empty(4096, device=dev, dtype=torch.float16)
+    code2, off = qs.state2.code, qs.offset
+    stream = torch.cuda.current_stream().cuda_stream
+    fn = _lib.lib.qz_gemv_4bit
+
+    def launch(i):
+        p, qa, a2 = sets[i % copies]
+        rc = fn(4096, 4096, x.data_ptr(), _lib.DT_F16, p.data_ptr(), _lib.NF4, 64, 0, qa.data_ptr(), a2.data_ptr(),
+                code2.data_ptr(), off.data_ptr(), 256, 0, 0, 0, y.data_ptr(), stream)
+        if rc:
+            raise RuntimeError(f"qz_gemv_4bit rc={rc}")
+
+    for i in range(2 * copies):
+        launch(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for i in range(iters):
+        ev[i][0].record()
+        launch(i)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    us = [a.elapsed_time(b) * 1e3 for a, b in ev]
+    # back-to-back throughput (includes launch gaps) for reference
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(iters):
+        launch(i)
+    e1.record()
+    torch.cuda.synchronize()
+    b2b_us = e0.elapsed_time(e1) * 1e3 / iters
+    return statistics.mean(us), statistics.median(us), b2b_us
+
+
+def cpu_baseline(target_s: float = 12.0):
+    import numpy as np
+
+    import oracle
+
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    g = torch.Generator().manual_seed(0)
+    W = (torch.randn(4096, 4096, generator=g) * 0.02).to(torch.float16)
+    x = torch.randn(4096, generator=g).to(torch.float16).float().numpy()
+    st = oracle.quantize_4bit(W.float().numpy(), 64, "nf4", double_quant=True)
+    oracle.cpu_dequant_matmul(x, st)  # warm-up
+    ts = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < target_s or len(ts) < 3:
+        t0 = time.perf_counter()
+        oracle.cpu_dequant_matmul(x, st)
+        ts.append(time.perf_counter() - t0)
+    layer_s = statistics.median(ts)
+    elems_per_token = LLAMA3_8B["num_hidden_layers"] * sum(m * k for m, k in LAYER_SHAPES)
+    tok_s = 1.0 / (layer_s * elems_per_token / (4096 * 4096))
+    del np
+    return {"value": round(tok_s, 5), "unit": "tokens/s", "cores": cores, "kind": "port",
+            "sample": f"config #1: Linear4bit(4096,4096) NF4+DQ CPU dequant + torch.matmul fp32 "
+                      f"(oracle restatement), median of {len(ts)} runs = {layer_s * 1e3:.1f} ms/layer, "
+                      f"scaled by elements to the 224 Linear4bit layers of one Llama-3-8B token"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=32)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    t_build = time.perf_counter()
+    model, cfg = build_model(args.layers, seed=0)
+    if world > 1:
+        from quantizations_amd.parallel import shard_model_linear4bit
+        shard_model_linear4bit(model, rank, world)
+        torch.cuda.empty_cache()
+    log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
+        f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
+
+    dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world)
+    t = torch.tensor([dt], device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    tok_s = args.steps / dt
+
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        del model
+        torch.cuda.empty_cache()
+        mean_us, med_us, b2b_us = gemv_roofline()
+        ach = GEMV_BYTES_4096 / (mean_us * 1e-6) / 1e9
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "gemv_4096_pmc.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_gemv_4bit<LUT16,DQ,f16,R=4,WK=2> 4096x4096 NF4+DQ",
+                "launch_us_mean": round(mean_us, 3), "launch_us_median": round(med_us, 3),
+                "back_to_back_us": round(b2b_us, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": "decode tokens/sec Llama-3-8B NF4 bs=1; 4096×4096 GEMV GB/s vs HBM peak",
+            "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
+            "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
+            "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
+                       "prompt_len": args.prompt, "batch": 1,
+                       "parallelism": "single" if world == 1 else f"rowsplit-tp{world}-allgather"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * quantizations.h -- C-ABI of libquantizations.so, the MI355X (gfx950) native
+ * 4-bit Linear4bit library.
+ *
+ * Drop-in boundary.  The reference exposes its kernels as the CPython module
+ * `kbkim_lib` (pythonInterface.cpp:154-178) whose five functions take raw
+ * device pointers as Python ints and integer sizes.  This header exports the
+ * SAME five names with the SAME argument order and meaning as plain
+ * `extern "C"` symbols, so any FFI (ctypes -- quantizations_amd/kbkim_lib.py --,
+ * cgo, JNI, N-API) can bind them.  Differences, all additive:
+ *   - every function returns an int status (0 = success, <0 = argument error,
+ *     >0 = hipError_t) instead of silently ignoring errors;
+ *   - `*_stream` variants take the HIP stream to launch on (the reference
+ *     launches on the legacy default stream, ops.cu:170);
+ *   - qz_* entry points expose the MI355X-native fused path (in-kernel double
+ *     quant, NF4, fp16/bf16/fp32 activations, fused bias, row-shard views).
+ *
+ * Ownership: every buffer is owned by the caller (torch in Python); the
+ * library never allocates, frees or synchronises.  Any workspace is passed in.
+ * All pointers are device pointers unless stated otherwise.
+ */
+#ifndef QUANTIZATIONS_H
+#define QUANTIZATIONS_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element dtypes */
+#define QZ_DT_F16 0
+#define QZ_DT_BF16 1
+#define QZ_DT_F32 2
+
+/* 4-bit codebooks */
+#define QZ_FP4 0 /* bnb FP4 (get_4bit_type("fp4"), core.py:208-229)         */
+#define QZ_NF4 1 /* NF4 codebook q_data (kernels.cu:851)                     */
+
+/* status codes (>0 values are hipError_t) */
+#define QZ_OK 0
+#define QZ_ERR_ARG (-1)       /* null pointer / negative size                 */
+#define QZ_ERR_BLOCKSIZE (-2) /* blocksize not in {64,...,4096} (core.py:549) */
+#define QZ_ERR_SHAPE (-3)     /* unsupported M/K/n combination               */
+#define QZ_ERR_DTYPE (-4)     /* unknown dtype / quant type                  */
+
+/* ------------------------------------------------------------------------ */
+/* Reference-compatible entry points (pythonInterface.cpp:34-46)            */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces gemm_4bit_inference_naive_fp32 (pythonInterface.cpp:34, kernel
+ * kernels.cu:1061-1219, launcher ops.cu:167-171).  out[m] = B[m,k] . A[k]
+ * with fp32 A/out, fp32 per-block absmax (already double-dequantised by the
+ * caller, core.py:467-468) and a 16-float device codebook `datatype`.
+ * n must be 1; lda/ldc are ignored (=m); ldb is the row stride in bytes
+ * ((k+1)/2, core.py:482). */
+int cgemm_4bit_inference_naive_fp32(int m, int n, int k, float *A, unsigned char *B, float *absmax,
+                                    float *datatype, float *out, int lda, int ldb, int ldc, int blocksize);
+
+/* Replaces quantizeBlockwise_fp16_fp4 (pythonInterface.cpp:37, kernels.cu:340-478
+ * with FP4): fp16 A[n] -> packed out[(n+1)/2] (high nibble = even element) and
+ * fp32 absmax[ceil(n/blocksize)].  `code` is unused (NULL in core.py:553). */
+int cquantize_blockwise_fp16_fp4(float *code, void *A, float *absmax, unsigned char *out, int blocksize, int n);
+
+/* Replaces dequantizeBlockwise_fp16_fp4 (pythonInterface.cpp:40, kernels.cu:554-560):
+ * packed A -> fp16 out[n] via the FP4 tree (code 8 -> -0.0). */
+int cdequantize_blockwise_fp16_fp4(float *code, unsigned char *A, float *absmax, void *out, int blocksize, int n);
+
+/* Replaces quantizeBlockwise_fp32 (pythonInterface.cpp:43, kernels.cu:340-478
+ * General8bit): fp32 A[n] -> u8 out[n] + fp32 absmax via the 256-entry code. */
+int cquantize_blockwise_fp32(float *code, float *A, float *absmax, unsigned char *out, int blocksize, int n);
+
+/* Replaces dequantizeBlockwise_fp32 (pythonInterface.cpp:46, kernels.cu:549-553):
+ * out[i] = code[A[i]] * absmax[i / blocksize]. */
+int cdequantize_blockwise_fp32(float *code, unsigned char *A, float *absmax, float *out, int blocksize, int n);
+
+/* Same five, launched on an explicit HIP stream (hipStream_t passed as void*). */
+int cgemm_4bit_inference_naive_fp32_stream(int m, int n, int k, float *A, unsigned char *B, float *absmax,
+                                           float *datatype, float *out, int lda, int ldb, int ldc, int blocksize,
+                                           void *stream);
+int cquantize_blockwise_fp16_fp4_stream(float *code, void *A, float *absmax, unsigned char *out, int blocksize, int n,
+                                        void *stream);
+int cdequantize_blockwise_fp16_fp4_stream(float *code, unsigned char *A, float *absmax, void *out, int blocksize,
+                                          int n, void *stream);
+int cquantize_blockwise_fp32_stream(float *code, float *A, float *absmax, unsigned char *out, int blocksize, int n,
+                                    void *stream);
+int cdequantize_blockwise_fp32_stream(float *code, unsigned char *A, float *absmax, float *out, int blocksize, int n,
+                                      void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* MI355X-native entry points                                               */
+/* ------------------------------------------------------------------------ */
+
+/* Per-block scale source shared by the 4-bit consumers (GEMV, GEMM, dequant).
+ * Exactly one of `absmax` (fp32[nb], no double quant) or `qabsmax` (u8[nb],
+ * double quant) is non-NULL.  With double quant the consumer computes, in
+ * kernel, absmax[b] = code2[qabsmax[b]] * absmax2[b / blocksize2] + *offset
+ * (two separately rounded fp32 ops, = core.py:467-468).  Block indices are
+ * global: b = block_base + (local flat element) / blocksize, so a row shard
+ * can pass the unsliced scale arrays with block_base = row0 * K / blocksize. */
+
+/* Fused 4-bit GEMV (decode, modules.py:56-61 -> core.py:426-504):
+ *   y[r] = sum_k x[k] * lut[nib(r,k)] * absmax[blk(r,k)]  (+ bias[r]),
+ * r in [0,M), B = packed rows (K/2 bytes each, high nibble first).
+ * x/bias/y share `dtype` (QZ_DT_*); accumulation is fp32.  `lut` (16 fp32,
+ * device) is optional: NULL selects the built-in codebook of `quant_type`. */
+int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type, int blocksize,
+                 const float *absmax, const unsigned char *qabsmax, const float *absmax2, const float *code2,
+                 const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
+                 void *y, void *stream);
+
+/* Fused 4-bit GEMM (prefill, modules.py:62-64): Y[T,M] = X[T,K] . W[M,K]^T
+ * (+ bias) with W dequantised tile-by-tile into LDS and multiplied on MFMA
+ * (fp16/bf16 in, fp32 accumulate).  X/Y/bias share `dtype` (F16 or BF16);
+ * ldx/ldy are row strides in elements. */
+int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dtype, const unsigned char *B, int quant_type,
+                 int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
+                 const float *code2, const float *offset, int blocksize2, const void *bias, void *Y, int ldy,
+                 void *stream);
+
+/* 4-bit blockwise quantisation (quantize_4bit, core.py:507-559): A[n] of
+ * `a_dtype` -> packed out[(n+1)/2] + fp32 absmax[ceil(n/blocksize)]. */
+int qz_quantize_4bit(const void *A, int a_dtype, long long n, int blocksize, int quant_type, float *absmax,
+                     unsigned char *out, void *stream);
+
+/* Deterministic mean of absmax[n] (core.py:563), fixed fp64 reduction tree
+ * (see DESIGN.md).  `workspace` must hold qz_absmax_mean_workspace(n) doubles. */
+long long qz_absmax_mean_workspace(long long n);
+int qz_absmax_mean(const float *absmax, long long n, double *workspace, float *offset, void *stream);
+
+/* 8-bit blockwise quantisation with the 256-entry code (quantize_blockwise,
+ * core.py:317-366).  If `subtract` (device fp32 scalar) is non-NULL the input
+ * is A[i] - *subtract, fusing core.py:564. */
+int qz_quantize_blockwise_8bit(const float *code, const float *A, long long n, int blocksize, const float *subtract,
+                               float *absmax, unsigned char *out, void *stream);
+
+/* 8-bit blockwise dequantisation (dequantize_blockwise, core.py:369-423);
+ * optional `offset` fuses core.py:468. */
+int qz_dequantize_blockwise_8bit(const float *code, const unsigned char *A, const float *absmax, long long n,
+                                 int blocksize, const float *offset, float *out, void *stream);
+
+/* 4-bit dequantisation to `out_dtype` (dequantize_4bit, core.py:581-631):
+ * FP4 through the dDequantizeFP4Tree semantics (code 8 -> -0.0), NF4 via its
+ * codebook; scale source as for qz_gemv_4bit (block_base = 0). */
+int qz_dequantize_4bit(const unsigned char *A, long long n, int quant_type, int blocksize, const float *absmax,
+                       const unsigned char *qabsmax, const float *absmax2, const float *code2, const float *offset,
+                       int blocksize2, void *out, int out_dtype, void *stream);
+
+/* Library/ABI version (major*10000 + minor*100 + patch). */
+int qz_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QUANTIZATIONS_H */

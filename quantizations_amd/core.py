@@ -1,0 +1,356 @@
+"""Functional 4-bit API -- same names, arguments and errors as the reference
+``core.py``, running on the MI355X-native kernels of libquantizations.so.
+
+Reference map (kkbwilldo/quantizations, core.py):
+  QuantState            :23-88     Params4bit           :91-190
+  get_4bit_type         :193-229   get_ptr              :232-248
+  create_dynamic_map    :251-314   quantize_blockwise   :317-366
+  dequantize_blockwise  :369-423   gemv_4bit            :426-504
+  quantize_4bit         :507-578   dequantize_4bit      :581-634
+
+What differs, on purpose (DESIGN.md "Host layer"):
+  * ``quant_type="nf4"`` is supported (the reference only knows "fp4").
+  * ``compress_statistics`` (bnb's name for double quant) is honoured; the
+    reference always double-quantises.
+  * ``gemv_4bit`` is ONE fused launch (scale rebuild, LUT decode, dot, cast,
+    bias) instead of dequantize_blockwise + ``+= offset`` + GEMV; no
+    per-call allocation besides the output.
+  * the absmax mean is a fixed-order fp64 reduction (deterministic), not
+    torch's fp32 ``mean()``.
+  * every launch goes to torch's current stream; failures raise.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from ._lib import check, dtype_code, lib, ptr
+
+name2qmap: dict = {}
+
+dtype2bytes = {torch.uint8: 1}
+
+_VALID_BLOCKSIZES = (4096, 2048, 1024, 512, 256, 128, 64)
+
+# NF4 codebook: reference csrc/kernels.cu:851 (q_data)
+NF4_CODE = [-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453, -0.28444138169288635,
+            -0.18477343022823334, -0.09105003625154495, 0.0, 0.07958029955625534, 0.16093020141124725,
+            0.24611230194568634, 0.33791524171829224, 0.44070982933044434, 0.5626170039176941,
+            0.7229568362236023, 1.0]
+
+
+class QuantState:
+    """Container of the 4-bit quantisation statistics (reference core.py:23-88)."""
+
+    valid_quant_types = ("fp4", "nf4")
+    valid_qs_keys = [
+        "absmax", "quant_map", "nested_absmax", "nested_quant_map", "quant_state", "quant_type",
+        "blocksize", "dtype", "shape", "nested_blocksize", "nested_dtype", "nested_offset",
+    ]
+
+    def __init__(self, absmax, shape=None, code=None, blocksize=None, quant_type=None, dtype=None, offset=None,
+                 state2=None):
+        self.absmax = absmax
+        self.shape = shape
+        self.code = code
+        self.dtype = dtype
+        self.blocksize = blocksize
+        self.quant_type = quant_type
+        self.offset = offset
+        self.state2 = state2
+        self.nested = state2 is not None
+
+    def to(self, device):
+        """Move the statistics to `device` (reference core.py:78-88; also valid without double quant)."""
+        self.absmax = self.absmax.to(device)
+        if self.code is not None:
+            self.code = self.code.to(device)
+        if self.nested:
+            self.offset = self.offset.to(device)
+            self.state2.absmax = self.state2.absmax.to(device)
+            self.state2.code = self.state2.code.to(device)
+
+    # -- scale-source view used by every 4-bit consumer --------------------
+    def scale_args(self):
+        """(absmax, qabsmax, absmax2, code2, offset, blocksize2) pointers for the C-ABI."""
+        if self.nested:
+            return (0, ptr(self.absmax), ptr(self.state2.absmax), ptr(self.state2.code), ptr(self.offset),
+                    int(self.state2.blocksize))
+        return (ptr(self.absmax), 0, 0, 0, 0, 0)
+
+    # -- serialisation (bnb-compatible key names, reference valid_qs_keys) --
+    def as_dict(self, packed: bool = False) -> dict:
+        d = {
+            "quant_type": self.quant_type,
+            "absmax": self.absmax,
+            "blocksize": self.blocksize,
+            "quant_map": self.code,
+            "dtype": str(self.dtype).replace("torch.", ""),
+            "shape": tuple(self.shape),
+        }
+        if self.nested:
+            d.update({
+                "nested_absmax": self.state2.absmax,
+                "nested_blocksize": self.state2.blocksize,
+                "nested_quant_map": self.state2.code,
+                "nested_dtype": str(self.state2.dtype).replace("torch.", ""),
+                "nested_offset": self.offset.item() if self.offset.numel() == 1 else self.offset,
+            })
+        return d
+
+    @classmethod
+    def from_dict(cls, qs_dict: dict, device) -> "QuantState":
+        d = dict(qs_dict)
+        state2 = None
+        offset = None
+        if "nested_absmax" in d:
+            state2 = cls(absmax=d["nested_absmax"].to(device), blocksize=int(d["nested_blocksize"]),
+                         code=d["nested_quant_map"].to(device), dtype=getattr(torch, d["nested_dtype"]))
+            off = d["nested_offset"]
+            offset = (off if isinstance(off, Tensor) else torch.tensor(float(off))).to(device=device,
+                                                                                       dtype=torch.float32)
+        return cls(quant_type=d["quant_type"], absmax=d["absmax"].to(device), blocksize=int(d["blocksize"]),
+                   code=d["quant_map"].to(device), dtype=getattr(torch, d["dtype"]), shape=torch.Size(d["shape"]),
+                   offset=offset, state2=state2)
+
+
+class Params4bit(torch.nn.Parameter):
+    """4-bit weight parameter (reference core.py:91-190); ``.to(cuda)`` quantises once."""
+
+    def __new__(cls, data: Optional[Tensor] = None, requires_grad=False, quant_state: Optional[QuantState] = None,
+                blocksize: int = 64, quant_type: str = "fp4", quant_storage: torch.dtype = torch.uint8,
+                module=None, bnb_quantized: bool = False, compress_statistics: bool = True, **_ignored):
+        if data is None:
+            data = torch.empty(0)
+        self = Tensor._make_subclass(cls, data, requires_grad)
+        self.blocksize = blocksize
+        self.quant_type = quant_type
+        self.quant_state = quant_state
+        self.quant_storage = quant_storage
+        self.bnb_quantized = bnb_quantized
+        self.compress_statistics = compress_statistics
+        self.data = data
+        self.module = module
+        return self
+
+    def _quantize(self, device):
+        w = self.data.contiguous().to(device)
+        w_4bit, quant_state = quantize_4bit(w, blocksize=self.blocksize, quant_type=self.quant_type,
+                                            quant_storage=self.quant_storage,
+                                            compress_statistics=self.compress_statistics)
+        self.data = w_4bit
+        self.quant_state = quant_state
+        if self.module is not None:
+            self.module.quant_state = quant_state
+        self.bnb_quantized = True
+        return self
+
+    def cuda(self, device=None, non_blocking: bool = False):
+        return self.to(device="cuda" if device is None else device, non_blocking=non_blocking)
+
+    def to(self, *args, **kwargs):
+        device, dtype, non_blocking, _ = torch._C._nn._parse_to(*args, **kwargs)
+        if device is not None and device.type == "cuda" and not self.bnb_quantized:
+            return self._quantize(device)
+        if self.quant_state is not None and device is not None:
+            self.quant_state.to(device)
+        new = Params4bit(super().to(device=device, dtype=dtype, non_blocking=non_blocking),
+                         requires_grad=self.requires_grad, quant_state=self.quant_state, blocksize=self.blocksize,
+                         quant_type=self.quant_type, quant_storage=self.quant_storage, module=self.module,
+                         bnb_quantized=self.bnb_quantized, compress_statistics=self.compress_statistics)
+        return new
+
+
+def get_4bit_type(typename, device=None, blocksize=64):
+    """16-entry codebook of `typename` (reference core.py:193-229; "nf4" = kernels.cu:851)."""
+    if device is None:
+        device = "cuda"
+    if typename == "fp4":
+        data = torch.tensor([0, 0.0625, 8.0, 12.0, 4.0, 6.0, 2.0, 3.0, -0, -0.0625, -8.0, -12.0, -4.0, -6.0, -2.0,
+                             -3.0], device=device)
+        data.div_(data.abs().max())
+        return data
+    if typename == "nf4":
+        return torch.tensor(NF4_CODE, dtype=torch.float32, device=device)
+    raise NotImplementedError(f"Typename {typename} not supported")
+
+
+def get_ptr(A: Optional[Tensor]) -> int:
+    """Device address of A, 0 for None (reference core.py:232-248)."""
+    return 0 if A is None else A.data.data_ptr()
+
+
+def create_dynamic_map(signed=True, max_exponent_bits=7, total_bits=8) -> Tensor:
+    """Signed dynamic 8-bit code (reference core.py:251-314): for exponent i, the
+    midpoints of linspace(0.1, 1, 2^i + 1) scaled by 10^(i-6), both signs, plus 0 and 1."""
+    values = []
+    non_sign_bits = total_bits - 1
+    for i in range(max_exponent_bits):
+        n = 2 ** (i + non_sign_bits - max_exponent_bits) + 1 if signed else \
+            2 ** (i + non_sign_bits - max_exponent_bits + 1) + 1
+        grid = torch.linspace(0.1, 1, int(n))
+        mids = (grid[:-1] + grid[1:]) / 2.0
+        scale = 10 ** (-(max_exponent_bits - 1) + i)
+        values.extend((scale * mids).tolist())
+        if signed:
+            values.extend((-scale * mids).tolist())
+    extra = 2 ** (non_sign_bits - max_exponent_bits) - 1
+    if extra > 0:
+        grid = torch.linspace(0.1, 1, extra + 1)
+        mids = (grid[:-1] + grid[1:]) / 2.0
+        scale = 10 ** (-(max_exponent_bits - 1) + max_exponent_bits - 1)
+        values.extend((scale * mids).tolist())
+        if signed:
+            values.extend((-scale * mids).tolist())
+    values.extend([0, 1.0])
+    assert len(values) == 2 ** total_bits
+    values.extend([0] * (256 - len(values)))
+    values.sort()
+    return Tensor(values)
+
+
+def _dynamic_code(device) -> Tensor:
+    key = ("dynamic", str(device))
+    if key not in name2qmap:
+        name2qmap[key] = create_dynamic_map().to(device)
+    return name2qmap[key]
+
+
+def _require_cuda(t: Tensor, what: str):
+    if t.device.type != "cuda":
+        raise NotImplementedError(f"Device type not supported for {what}: {t.device.type}")
+
+
+def quantize_blockwise(A: Tensor, blocksize=4096, offset: Optional[Tensor] = None) -> Tuple[Tensor, QuantState]:
+    """8-bit blockwise quantisation with the dynamic code (reference core.py:317-366).
+    `offset` (device scalar) fuses the reference's preceding ``A -= offset``."""
+    _require_cuda(A, "blockwise quantization")
+    assert blocksize in _VALID_BLOCKSIZES
+    code = _dynamic_code(A.device)
+    n = A.numel()
+    blocks = (n + blocksize - 1) // blocksize
+    absmax = torch.zeros((blocks,), device=A.device, dtype=torch.float32)
+    out = torch.zeros_like(A, dtype=torch.uint8)
+    A = A.contiguous().float()
+    check(lib.qz_quantize_blockwise_8bit(ptr(code), ptr(A), n, blocksize, ptr(offset), ptr(absmax), ptr(out),
+                                         _lib.stream_of(A)), "quantize_blockwise")
+    return out, QuantState(absmax=absmax, code=code, blocksize=blocksize, dtype=torch.float32)
+
+
+def dequantize_blockwise(A: Tensor, quant_state: Optional[QuantState] = None, absmax: Optional[Tensor] = None,
+                         code: Optional[Tensor] = None, out: Optional[Tensor] = None, blocksize: int = 4096,
+                         nested=False, offset: Optional[Tensor] = None) -> Tensor:
+    """Inverse of quantize_blockwise (reference core.py:369-423); `offset` fuses ``+= offset``."""
+    assert quant_state is not None or absmax is not None
+    if quant_state is None:
+        quant_state = QuantState(absmax=absmax, code=code if code is not None else _dynamic_code(A.device),
+                                 blocksize=blocksize, dtype=torch.float32)
+    if quant_state.blocksize not in _VALID_BLOCKSIZES:
+        raise ValueError(f"The blockwise of {quant_state.blocksize} is not supported. "
+                         f"Supported values: [2048, 4096, 1024, 512, 256, 128, 64]")
+    if out is None:
+        out = torch.empty(A.shape, dtype=torch.float32, device=A.device)
+    check(lib.qz_dequantize_blockwise_8bit(ptr(quant_state.code), ptr(A), ptr(quant_state.absmax), A.numel(),
+                                           quant_state.blocksize, ptr(offset), ptr(out), _lib.stream_of(A)),
+          "dequantize_blockwise")
+    return out
+
+
+def quantize_4bit(A: Tensor, blocksize=64, quant_type="fp4", quant_storage=torch.uint8,
+                  compress_statistics: bool = True) -> Tuple[Tensor, QuantState]:
+    """Blockwise 4-bit quantisation (reference core.py:507-578): pack two codes per
+    byte (high nibble first), then -- with double quant -- offset = mean(absmax)
+    and an 8-bit blockwise code of absmax - offset with blocksize 256."""
+    _require_cuda(A, "FP4 quantization")
+    if quant_type not in QuantState.valid_quant_types:
+        raise NotImplementedError(f"4-bit quantization data type {quant_type} is not implemented.")
+    assert blocksize in _VALID_BLOCKSIZES
+    if quant_storage != torch.uint8:
+        raise NotImplementedError(f"quant_storage {quant_storage} is not supported (uint8 only)")
+    n = A.numel()
+    input_shape = A.shape
+    A = A.contiguous()
+    s = _lib.stream_of(A)
+    blocks = (n + blocksize - 1) // blocksize
+    absmax = torch.zeros((blocks,), device=A.device, dtype=torch.float32)
+    out = torch.zeros(((n + 1) // 2, 1), dtype=torch.uint8, device=A.device)
+    check(lib.qz_quantize_4bit(ptr(A), dtype_code(A.dtype), n, blocksize, _lib.QUANT_TYPES[quant_type], ptr(absmax),
+                               ptr(out), s), "quantize_4bit")
+    code = get_4bit_type(quant_type, device=A.device)
+    if not compress_statistics:
+        return out, QuantState(absmax=absmax, shape=input_shape, dtype=A.dtype, blocksize=blocksize, code=code,
+                               quant_type=quant_type)
+    offset = torch.empty((), device=A.device, dtype=torch.float32)
+    ws = torch.empty(int(lib.qz_absmax_mean_workspace(blocks)), device=A.device, dtype=torch.float64)
+    check(lib.qz_absmax_mean(ptr(absmax), blocks, ptr(ws), ptr(offset), s), "absmax mean")
+    qabsmax, state2 = quantize_blockwise(absmax, blocksize=256, offset=offset)
+    del absmax
+    return out, QuantState(absmax=qabsmax, shape=input_shape, dtype=A.dtype, blocksize=blocksize, code=code,
+                           quant_type=quant_type, offset=offset, state2=state2)
+
+
+def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, blocksize: int = 64, quant_type="fp4",
+                    out_dtype: Optional[torch.dtype] = None) -> Tensor:
+    """Full-weight dequantisation (reference core.py:581-634); returns ``out.t()``
+    like the reference.  FP4 follows the dDequantizeFP4Tree semantics."""
+    if blocksize not in _VALID_BLOCKSIZES:
+        raise ValueError(f"The blockwise of {blocksize} is not supported. "
+                         f"Supported values: [2048, 4096, 1024, 512, 256, 128, 64]")
+    qt = quant_state.quant_type or quant_type
+    if qt not in QuantState.valid_quant_types:
+        raise NotImplementedError(f"4-bit quantization data type {qt} is not implemented.")
+    dt = out_dtype or quant_state.dtype
+    out = torch.empty(quant_state.shape, dtype=dt, device=A.device)
+    check(lib.qz_dequantize_4bit(ptr(A), out.numel(), _lib.QUANT_TYPES[qt], quant_state.blocksize,
+                                 *quant_state.scale_args(), ptr(out), dtype_code(dt), _lib.stream_of(A)),
+          "dequantize_4bit")
+    return out.t()
+
+
+def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
+              state=None, bias: Optional[Tensor] = None, block_base: int = 0) -> Tensor:
+    """Batch-1 4-bit GEMV (reference core.py:426-504) as ONE fused kernel:
+    y = x . W^T (+ bias), W from `state`; out dtype = A.dtype."""
+    if state is None:
+        raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
+    if A.numel() != A.shape[-1]:
+        raise ValueError('Dimensions of A are invalid. Must be a vector with the leading dimensions of "1", '
+                         'e.g. [1, 1, 2048]')
+    M, K = state.shape[0], state.shape[1]
+    if A.shape[-1] != K:
+        raise ValueError(f"A has {A.shape[-1]} features, the 4-bit weight expects {K}")
+    if out is None:
+        shape = (A.shape[0], A.shape[1], M) if A.dim() == 3 else (A.shape[0], M) if A.dim() == 2 else (M,)
+        out = torch.empty(shape, dtype=A.dtype, device=A.device)
+    A = A.contiguous()
+    if bias is not None and bias.dtype != A.dtype:
+        bias = bias.to(A.dtype)
+    check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _lib.QUANT_TYPES[state.quant_type],
+                           state.blocksize, *state.scale_args(), block_base, 0, ptr(bias), ptr(out),
+                           _lib.stream_of(A)), "gemv_4bit")
+    return out
+
+
+def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = None) -> Tensor:
+    """Batched (prefill) 4-bit GEMM: A[..., K] . W^T -> [..., M] on the fused MFMA
+    kernel when supported (fp16, K % 64 == 0), otherwise the reference's route
+    (dequantize_4bit + torch GEMM)."""
+    M, K = state.shape[0], state.shape[1]
+    lead = A.shape[:-1]
+    A2 = A.reshape(-1, K)
+    if A2.stride(-1) != 1 or A2.data_ptr() % 16 != 0:
+        A2 = A2.contiguous()
+    T = A2.shape[0]
+    if A.dtype == torch.float16 and K % 64 == 0 and state.blocksize % 64 == 0 and A2.stride(0) % 8 == 0:
+        out = torch.empty((T, M), dtype=A.dtype, device=A.device)
+        if bias is not None and bias.dtype != A.dtype:
+            bias = bias.to(A.dtype)
+        check(lib.qz_gemm_4bit(T, M, K, ptr(A2), A2.stride(0), _lib.DT_F16, ptr(B),
+                               _lib.QUANT_TYPES[state.quant_type], state.blocksize, *state.scale_args(), ptr(bias),
+                               ptr(out), M, _lib.stream_of(A)), "gemm_4bit")
+        return out.reshape(*lead, M)
+    W = dequantize_4bit(B, state).t()
+    return torch.nn.functional.linear(A, W.to(A.dtype), bias)

@@ -1,0 +1,492 @@
+// gemv.hip -- fused 4-bit dequantise + GEMV for batch-1 decode on gfx950.
+//
+// Replaces the reference decode chain (modules.py:56-61 -> core.py:426-504):
+// absmax double-dequant kernel + `+= offset` + kgemm_4bit_inference_naive
+// (kernels.cu:1061-1219) + two cast kernels, with ONE launch.
+//
+// Layout (unchanged bnb/reference format): W is [M, K] row-major, two 4-bit
+// codes per byte, high nibble = even element; one scale per `blocksize`
+// consecutive flat elements; with double quant the scale is rebuilt in kernel
+// as code2[q] * absmax2[b / 256] + offset (two roundings, as core.py:467-468).
+//
+// Work decomposition (wave64-first): a K-STEP is 1 KiB of one row = 2048
+// elements; lane l of a wave owns bytes [16 l, 16 l + 16) of the step, i.e.
+// 32 consecutive elements that always sit inside one scale block.  A wave
+// handles R rows of one step at a time, so its 64 B slice of x (fp16) is
+// loaded once and reused R times; the 4 waves of a 256-thread workgroup are
+// split WK ways along K (steps s = wk, wk+WK, ...) and RG = 4/WK ways along
+// rows, and the WK partial sums meet in LDS.  Weight loads are 16 B/lane
+// (1 KiB per wave instruction, fully coalesced) and non-temporal: each byte
+// is read exactly once per call.
+//
+// Nibble decode happens in VALU registers with v_perm_b32 byte lookups
+// (no LDS, no bank conflicts):
+//  * FP4 (sign/magnitude codebook): the 8 magnitudes x12 = {0,1/16,8,12,4,6,
+//    2,3} are exact in fp16 and all have a zero low byte, so one v_perm per 4
+//    nibbles yields the fp16 high bytes, the sign bit is OR-ed in, and one
+//    more v_perm per pair assembles half2 (e_2j, e_2j+1).  The x12 is undone
+//    once per output.  ~2 VALU ops per weight.
+//  * 16-entry codebooks (NF4, or any runtime codebook): fp16 low/high byte
+//    tables, two v_perm (entries 0-7 / 8-15) blended by v_bfi on bit 3,
+//    then pairs (e0,e2),(e4,e6),(e1,e3),(e5,e7) -- x is pre-permuted to match
+//    once per step.  ~3.5 VALU ops per weight.
+// Products: v_dot2_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
+// per 32-element chunk the fp32 dot is scaled by the block absmax with one
+// FMA.  fp32/bf16 activations are split into hi+lo fp16 halves (x = xh + xl,
+// 2^-22 relative) so they keep fp32-class accuracy.
+#include "common.h"
+
+namespace qz {
+
+enum { kModeFP4 = 0, kModeLUT16 = 1 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct GemvParams {
+  const unsigned char *B;
+  const void *x;
+  ScaleSrc sc;
+  const void *bias;
+  void *y;
+  const float *lut;  // runtime 16-entry codebook (kModeLUT16) or nullptr
+  long long block_base;
+  int M, K;
+  int bs_log2, bs2_log2;
+  float out_scale;
+  uint32_t tab[8];
+};
+
+__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  return __builtin_amdgcn_perm(s0, s1, sel);
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, a), __builtin_bit_cast(h2_t, b), c, false);
+}
+
+// FP4: 8 nibbles -> 4 half2 in natural order P[j] = (e_2j, e_2j+1), values x12.
+__device__ __forceinline__ void decode_fp4(uint32_t w, uint32_t t0, uint32_t t1, uint32_t (&P)[4]) {
+  const uint32_t hh = perm(t1, t0, (w >> 4) & 0x07070707u) | (w & 0x80808080u);
+  const uint32_t hl = perm(t1, t0, w & 0x07070707u) | ((w << 4) & 0x80808080u);
+  P[0] = perm(hh, hl, 0x000C040Cu);
+  P[1] = perm(hh, hl, 0x010C050Cu);
+  P[2] = perm(hh, hl, 0x020C060Cu);
+  P[3] = perm(hh, hl, 0x030C070Cu);
+}
+
+// 16-entry codebook: 8 nibbles -> (e0,e2),(e4,e6),(e1,e3),(e5,e7).
+__device__ __forceinline__ void decode_lut16(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
+  const uint32_t sh = (w >> 4) & 0x07070707u;
+  const uint32_t mh = perm(w << 8, w, 0x090B080Au);  // 0xFF per byte where the high nibble has bit 3
+  const uint32_t lh = bfi(mh, perm(t[3], t[2], sh), perm(t[1], t[0], sh));
+  const uint32_t hh = bfi(mh, perm(t[7], t[6], sh), perm(t[5], t[4], sh));
+  const uint32_t w4 = w << 4;
+  const uint32_t sl = w & 0x07070707u;
+  const uint32_t ml = perm(w4 << 8, w4, 0x090B080Au);
+  const uint32_t ll = bfi(ml, perm(t[3], t[2], sl), perm(t[1], t[0], sl));
+  const uint32_t hl = bfi(ml, perm(t[7], t[6], sl), perm(t[5], t[4], sl));
+  P[0] = perm(hh, lh, 0x05010400u);
+  P[1] = perm(hh, lh, 0x07030602u);
+  P[2] = perm(hl, ll, 0x05010400u);
+  P[3] = perm(hl, ll, 0x07030602u);
+}
+
+// x slice of one lane for one step: 32 elements as 16 half2 "hi" (and "lo"
+// for fp32/bf16 activations), arranged in the pair order of MODE.
+template <int MODE, int DT> struct XSlice {
+  static constexpr bool kSplit = DT != QZ_DT_F16;
+  uint32_t hi[16];
+  uint32_t lo[kSplit ? 16 : 1];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) hi[i] = 0;
+    if constexpr (kSplit) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) lo[i] = 0;
+    }
+  }
+
+  __device__ __forceinline__ void load(const void *x, long long e0) {
+    if constexpr (DT == QZ_DT_F16) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(x) + e0);
+      uint32_t n[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = p[i];
+        n[4 * i] = v.x; n[4 * i + 1] = v.y; n[4 * i + 2] = v.z; n[4 * i + 3] = v.w;
+      }
+      if constexpr (MODE == kModeFP4) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) hi[i] = n[i];
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {  // per 8 elements: (x0,x2),(x4,x6),(x1,x3),(x5,x7)
+          hi[4 * d + 0] = perm(n[4 * d + 1], n[4 * d + 0], 0x05040100u);
+          hi[4 * d + 1] = perm(n[4 * d + 3], n[4 * d + 2], 0x05040100u);
+          hi[4 * d + 2] = perm(n[4 * d + 1], n[4 * d + 0], 0x07060302u);
+          hi[4 * d + 3] = perm(n[4 * d + 3], n[4 * d + 2], 0x07060302u);
+        }
+      }
+    } else {
+      float f[32];
+      if constexpr (DT == QZ_DT_F32) {
+        const float4 *p = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(x) + e0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float4 v = p[i];
+          f[4 * i] = v.x; f[4 * i + 1] = v.y; f[4 * i + 2] = v.z; f[4 * i + 3] = v.w;
+        }
+      } else {
+        const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(x) + e0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint4 v = p[i];
+          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f[8 * i + 2 * j] = __uint_as_float(u[j] << 16);
+            f[8 * i + 2 * j + 1] = __uint_as_float(u[j] & 0xFFFF0000u);
+          }
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        int a[4], b[4];
+        if constexpr (MODE == kModeFP4) {
+          a[0] = 0; b[0] = 1; a[1] = 2; b[1] = 3; a[2] = 4; b[2] = 5; a[3] = 6; b[3] = 7;
+        } else {
+          a[0] = 0; b[0] = 2; a[1] = 4; b[1] = 6; a[2] = 1; b[2] = 3; a[3] = 5; b[3] = 7;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float fa = f[8 * d + a[j]], fb = f[8 * d + b[j]];
+          // hi = rtz(f) (never overflows to inf below 65536), lo = rtz(f - hi); f - hi is exact
+          const auto h = __builtin_amdgcn_cvt_pkrtz(fa, fb);
+          const float ra = fa - (float)h.x, rb = fb - (float)h.y;
+          hi[4 * d + j] = __builtin_bit_cast(uint32_t, h);
+          lo[4 * d + j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(ra, rb));
+        }
+      }
+    }
+  }
+};
+
+// dot of one lane's 16-byte weight chunk (32 codes) with its x slice
+template <int MODE, int DT>
+__device__ __forceinline__ float chunk_dot(const u32x4 &wv, const XSlice<MODE, DT> &xs, const uint32_t (&t)[8]) {
+  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+  float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t P[4];
+    if constexpr (MODE == kModeFP4) decode_fp4(w[d], t[0], t[1], P);
+    else decode_lut16(w[d], t, P);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j & 1) s1 = dot2(P[j], xs.hi[4 * d + j], s1);
+      else s0 = dot2(P[j], xs.hi[4 * d + j], s0);
+      if constexpr (XSlice<MODE, DT>::kSplit) {
+        if (j & 1) s1 = dot2(P[j], xs.lo[4 * d + j], s1);
+        else s0 = dot2(P[j], xs.lo[4 * d + j], s0);
+      }
+    }
+  }
+  return s0 + s1;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// One step's worth of loads for R rows (issued together, consumed later).
+template <int MODE, bool DQ, int DT, int R> struct StepLoads {
+  u32x4 wv[R];
+  uint32_t q[R];    // DQ: 8-bit scale code
+  float a[R];       // DQ: absmax2 entry; else: fp32 absmax
+  XSlice<MODE, DT> xs;
+
+  __device__ __forceinline__ void issue(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
+    const int boff = (s << 10) + (lane << 4);
+    const bool on = boff < row_bytes;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int row = row0 + r;
+      const bool ok = on && row < p.M;
+      const long long e = (long long)row * p.K + 2 * boff;
+      const long long b = p.block_base + (e >> p.bs_log2);
+      if (ok) {
+        wv[r] = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4 *>(p.B + (size_t)row * (size_t)row_bytes + (size_t)boff));
+        if constexpr (DQ) {
+          q[r] = p.sc.qabsmax[b];
+          a[r] = p.sc.absmax2[b >> p.bs2_log2];
+        } else {
+          a[r] = p.sc.absmax[b];
+        }
+      } else {
+        wv[r] = u32x4{0u, 0u, 0u, 0u};
+        q[r] = 0;
+        a[r] = 0.0f;
+      }
+    }
+    if (on) xs.load(p.x, 2LL * boff);
+    else xs.zero();
+  }
+};
+
+template <int MODE, bool DQ, int DT, int R, int WK>
+__global__ __launch_bounds__(256) void k_gemv_4bit(GemvParams p) {
+  constexpr int RG = 4 / WK;
+  __shared__ float s_code2[DQ ? 256 : 1];
+  __shared__ float s_part[4][R];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int wk = wave % WK;
+  const int rg = wave / WK;
+  const int row0 = (blockIdx.x * RG + rg) * R;
+  const int row_bytes = p.K >> 1;
+  const int nsteps = (row_bytes + 1023) >> 10;
+
+  // issue the first step's HBM loads before anything that waits
+  StepLoads<MODE, DQ, DT, R> cur;
+  int s = wk;
+  if (s < nsteps) cur.issue(p, row0, s, lane, row_bytes);
+
+  float offset = 0.0f;
+  if constexpr (DQ) {
+    s_code2[threadIdx.x] = p.sc.code2[threadIdx.x];
+    offset = *p.sc.offset;
+    __syncthreads();
+  }
+
+  uint32_t t[8];
+  if (p.lut) {  // runtime codebook -> fp16 byte tables (wave-uniform, once)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t h = __half_as_ushort(__float2half_rn(p.lut[i]));
+      t[i >> 2] |= (h & 0xFFu) << (8 * (i & 3));
+      t[4 + (i >> 2)] |= (h >> 8) << (8 * (i & 3));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
+  }
+
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+
+  for (; s < nsteps; s += WK) {
+    StepLoads<MODE, DQ, DT, R> nxt;
+    const bool more = s + WK < nsteps;
+    if (more) nxt.issue(p, row0, s + WK, lane, row_bytes);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float am;
+      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cur.q[r]], cur.a[r]), offset);
+      else am = cur.a[r];
+      acc[r] = fmaf(chunk_dot<MODE, DT>(cur.wv[r], cur.xs, t), am, acc[r]);
+    }
+    if (more) cur = nxt;
+  }
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float v = wave_sum(acc[r]);
+    if (lane == 0) s_part[wave][r] = v;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < RG * R) {
+    const int g = threadIdx.x / R, r = threadIdx.x % R;
+    const int row = (blockIdx.x * RG + g) * R + r;
+    if (row < p.M) {
+      float v = 0.0f;
+#pragma unroll
+      for (int k = 0; k < WK; ++k) v += s_part[g * WK + k][r];
+      v *= p.out_scale;
+      if (p.bias) v += load_f32<DT>(p.bias, row);
+      store_f32<DT>(p.y, row, v);
+    }
+  }
+}
+
+// Generic path for shapes the vector kernel does not cover (K % 32 != 0,
+// odd K, blocksize < 32): one wave per row, flat element addressing exactly
+// as the reference (e = r*K + k, byte e>>1, high nibble for even e).
+template <bool DQ, int DT>
+__global__ __launch_bounds__(256) void k_gemv_4bit_generic(GemvParams p, int quant_type) {
+  __shared__ float s_lut[16];
+  if (threadIdx.x < 16) s_lut[threadIdx.x] = p.lut ? p.lut[threadIdx.x] : 0.0f;
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = blockIdx.x * 4 + threadIdx.x / kWave;
+  if (row >= p.M) return;
+  const float offset = DQ ? *p.sc.offset : 0.0f;
+  float acc = 0.0f;
+  for (int k = lane; k < p.K; k += kWave) {
+    const long long e = (long long)row * p.K + k;
+    const uint32_t byte = p.B[e >> 1];
+    const uint32_t nib = (e & 1) ? (byte & 0xFu) : (byte >> 4);
+    const long long b = p.block_base + (e >> p.bs_log2);
+    float am;
+    if constexpr (DQ) am = __fadd_rn(__fmul_rn(p.sc.code2[p.sc.qabsmax[b]], p.sc.absmax2[b >> p.bs2_log2]), offset);
+    else am = p.sc.absmax[b];
+    float c;
+    if (p.lut) c = s_lut[nib];
+    else if (quant_type == QZ_NF4) c = kNF4[nib];
+    else c = (nib & 8u ? -1.0f : 1.0f) * dequant_fp4_tree(nib & 7u, 1.0f);
+    acc = fmaf(load_f32<DT>(p.x, k), __fmul_rn(c, am), acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    if (p.bias) acc += load_f32<DT>(p.bias, row);
+    store_f32<DT>(p.y, row, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side table construction
+// ---------------------------------------------------------------------------
+static uint16_t f32_to_f16_bits(float f) {
+  return __half_as_ushort(__float2half_rn(f));  // host-side RNE conversion (hip_fp16.h)
+}
+
+static void build_tables(int mode, int quant_type, uint32_t tab[8], float *out_scale) {
+  for (int i = 0; i < 8; ++i) tab[i] = 0;
+  if (mode == kModeFP4) {
+    // magnitudes x12 for codes 0..7: {0, 1/16, 8, 12, 4, 6, 2, 3}, fp16 high bytes (low bytes are 0)
+    const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};
+    for (int i = 0; i < 8; ++i) tab[i >> 2] |= (uint32_t)hb[i] << (8 * (i & 3));
+    *out_scale = 1.0f / 12.0f;
+    return;
+  }
+  static const float nf4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+                                0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
+                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                                0.7229568362236023f, 1.0f};
+  (void)quant_type;
+  for (int i = 0; i < 16; ++i) {
+    const uint16_t h = f32_to_f16_bits(nf4[i]);
+    tab[i >> 2] |= (uint32_t)(h & 0xFF) << (8 * (i & 3));
+    tab[4 + (i >> 2)] |= (uint32_t)(h >> 8) << (8 * (i & 3));
+  }
+  *out_scale = 1.0f;
+}
+
+static int ilog2(long long v) {
+  int l = 0;
+  while ((1LL << l) < v) ++l;
+  return (1LL << l) == v ? l : -1;
+}
+
+template <int MODE, bool DQ, int DT>
+static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
+  const int RG = 4 / WK;
+  const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
+#define QZ_GV(RR, WW) \
+  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW>), dim3(grid), dim3(256), 0, s, p)
+  if (WK == 4) {
+    if (R == 4) QZ_GV(4, 4); else if (R == 2) QZ_GV(2, 4); else QZ_GV(1, 4);
+  } else if (WK == 2) {
+    if (R == 4) QZ_GV(4, 2); else if (R == 2) QZ_GV(2, 2); else QZ_GV(1, 2);
+  } else {
+    if (R == 4) QZ_GV(4, 1); else if (R == 2) QZ_GV(2, 1); else QZ_GV(1, 1);
+  }
+#undef QZ_GV
+}
+
+template <int MODE, bool DQ>
+static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_t s) {
+  switch (dtype) {
+    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32>(p, R, WK, s); return QZ_OK;
+  }
+  return QZ_ERR_DTYPE;
+}
+
+}  // namespace qz
+
+using namespace qz;
+
+// Geometry choice shared with the Python side (quantizations_amd/core.py
+// documents it): WK = waves along K (<= steps), R = rows per wave, the largest
+// R that still gives >= 2048 waves (8 per CU) so that every CU keeps >= 32 KiB
+// of weight loads in flight.
+static void choose_geometry(int M, int K, int *R, int *WK) {
+  const int nsteps = ((K >> 1) + 1023) >> 10;
+  *WK = nsteps >= 4 ? 4 : (nsteps >= 2 ? 2 : 1);
+  *R = 1;
+  for (int r = 4; r >= 2; r >>= 1)
+    if ((long long)((M + r - 1) / r) * (*WK) >= 2048) {
+      *R = r;
+      break;
+    }
+}
+
+extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
+                            int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
+                            const float *code2, const float *offset, int blocksize2, long long block_base,
+                            const float *lut, const void *bias, void *y, void *stream) {
+  if (!x || !B || !y || M < 0 || K < 0) return QZ_ERR_ARG;
+  if ((absmax == nullptr) == (qabsmax == nullptr)) return QZ_ERR_ARG;
+  const bool dq = qabsmax != nullptr;
+  if (dq && (!absmax2 || !code2 || !offset)) return QZ_ERR_ARG;
+  if (quant_type != QZ_FP4 && quant_type != QZ_NF4) return QZ_ERR_DTYPE;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16 && dtype != QZ_DT_F32) return QZ_ERR_DTYPE;
+  const int bsl = ilog2(blocksize);
+  const int bs2l = dq ? ilog2(blocksize2) : 0;
+  if (bsl < 1 || bs2l < 0) return QZ_ERR_BLOCKSIZE;
+  if (M == 0) return QZ_OK;
+  hipStream_t s = (hipStream_t)stream;
+
+  GemvParams p;
+  p.B = B;
+  p.x = x;
+  p.sc = ScaleSrc{absmax, qabsmax, absmax2, code2, offset, blocksize2};
+  p.bias = bias;
+  p.y = y;
+  p.lut = lut;
+  p.block_base = block_base;
+  p.M = M;
+  p.K = K;
+  p.bs_log2 = bsl;
+  p.bs2_log2 = bs2l;
+
+  const bool vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 &&
+                      (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(x) % 16) == 0;
+  if (!vec_ok) {
+    const unsigned grid = (unsigned)((M + 3) / 4);
+    if (K == 0) return QZ_ERR_SHAPE;
+#define QZ_GG(DQ_, DT_) \
+  hipLaunchKernelGGL((k_gemv_4bit_generic<DQ_, DT_>), dim3(grid), dim3(256), 0, s, p, quant_type)
+    if (dq) {
+      if (dtype == QZ_DT_F16) QZ_GG(true, QZ_DT_F16); else if (dtype == QZ_DT_BF16) QZ_GG(true, QZ_DT_BF16); else QZ_GG(true, QZ_DT_F32);
+    } else {
+      if (dtype == QZ_DT_F16) QZ_GG(false, QZ_DT_F16); else if (dtype == QZ_DT_BF16) QZ_GG(false, QZ_DT_BF16); else QZ_GG(false, QZ_DT_F32);
+    }
+#undef QZ_GG
+    QZ_LAUNCH_CHECK();
+    return QZ_OK;
+  }
+
+  int R, WK;
+  choose_geometry(M, K, &R, &WK);
+  const int mode = (lut == nullptr && quant_type == QZ_FP4) ? kModeFP4 : kModeLUT16;
+  build_tables(mode, quant_type, p.tab, &p.out_scale);
+  int rc;
+  if (mode == kModeFP4) rc = dq ? dispatch_dt<kModeFP4, true>(p, dtype, R, WK, s) : dispatch_dt<kModeFP4, false>(p, dtype, R, WK, s);
+  else rc = dq ? dispatch_dt<kModeLUT16, true>(p, dtype, R, WK, s) : dispatch_dt<kModeLUT16, false>(p, dtype, R, WK, s);
+  if (rc != QZ_OK) return rc;
+  QZ_LAUNCH_CHECK();
+  return QZ_OK;
+}

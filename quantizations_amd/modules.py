@@ -1,0 +1,76 @@
+"""``Linear4bit`` -- drop-in for ``bnb.nn.Linear4bit`` / the reference
+``modules.Linear4bit`` (reference modules.py:67-151), inference only.
+
+Dispatch (reference modules.py:28-64): a single-token input
+(``A.numel() == A.shape[-1]``) runs the fused decode GEMV; anything else runs
+the fused prefill GEMM (MFMA).  Both consume the 4-bit weight directly -- no
+dequantised copy of W is ever materialised in HBM on the supported shapes.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .core import Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemv_4bit
+
+
+def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None):
+    """x . W^T (+ bias) for a 4-bit W (reference modules.py:28-64).  `B` is the packed
+    weight (the reference passes ``weight.t()``; only its storage is used)."""
+    assert quant_state is not None
+    if A.numel() == A.shape[-1]:
+        return gemv_4bit(A, B, out, state=quant_state, bias=bias)
+    return gemm_4bit(A, B, quant_state, bias=bias)
+
+
+class Linear4bit(nn.Linear):
+    """4-bit linear layer with the bnb / reference constructor signature
+    (reference modules.py:86-96).  ``quant_type`` is "fp4" or "nf4";
+    ``compress_statistics`` toggles double quantisation of the absmax."""
+
+    def __init__(self, input_features, output_features, bias=False, compute_dtype=None, compress_statistics=True,
+                 quant_type="fp4", quant_storage=torch.uint8, device=None):
+        super().__init__(input_features, output_features, bias, device)
+        self.weight = Params4bit(self.weight.data, requires_grad=False, quant_type=quant_type,
+                                 quant_storage=quant_storage, module=self, compress_statistics=compress_statistics)
+        self.compute_dtype = compute_dtype
+        self.compute_type_is_set = False
+        self.quant_state = None
+        self.quant_storage = quant_storage
+
+    def set_compute_type(self, x):
+        """Reference modules.py:112-122: fp32/bf16 inputs select their own dtype."""
+        if x.dtype in [torch.float32, torch.bfloat16]:
+            self.compute_dtype = x.dtype
+
+    def _input(self, x: torch.Tensor) -> torch.Tensor:
+        # The reference casts x to compute_dtype before the matmul (modules.py:141-142).
+        # Our kernels always accumulate in fp32, so an up-cast (e.g. fp16 -> fp32) is
+        # exact and skipped; a narrowing cast (e.g. fp16 -> bf16) changes values and
+        # is applied to keep the reference's numerics.
+        cd = self.compute_dtype
+        if cd is None or cd == x.dtype or cd == torch.float32:
+            return x
+        return x.to(cd)
+
+    def forward(self, x: torch.Tensor):
+        if not self.compute_type_is_set:
+            self.set_compute_type(x)
+            self.compute_type_is_set = True
+        qs = self.weight.quant_state
+        if qs is None:
+            raise RuntimeError("Linear4bit weight is not quantised yet: move the module to a GPU first")
+        inp_dtype = x.dtype
+        xin = self._input(x)
+        bias = None if self.bias is None else self.bias.to(xin.dtype)
+        out = matmul_4bit(xin, self.weight, bias=bias, quant_state=qs)
+        return out if out.dtype == inp_dtype else out.to(inp_dtype)
+
+    def dequantize(self) -> torch.Tensor:
+        """Dense weight [out, in] in the original dtype (for checks and export)."""
+        return dequantize_4bit(self.weight, self.weight.quant_state).t()
+
+    @property
+    def native_lib(self) -> str:
+        return _lib.LIB_PATH

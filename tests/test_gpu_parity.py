@@ -1,0 +1,407 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the CPU oracle and the
+committed golden vectors.
+
+Bars (DESIGN.md "Parity"):
+  * 4-bit codes, 8-bit double-quant codes, absmax, absmax2, offset: bit-exact.
+  * dequantised weights (fp16/bf16/fp32 stores of fp32 products): bit-exact.
+  * GEMV / GEMM outputs: ||y - y_ref||_2 / ||y_ref||_2 <= 1e-3 and
+    |y - y_ref| <= 1e-3 * max|y_ref| + 1 ulp(out dtype), y_ref = fp64 sum of the
+    reference's fp32 weight products (oracle.gemv) -- SURVEY.md appendix A.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda")
+REL_TOL = 1e-3
+
+
+def _w(M, K, seed=0, dtype=torch.float16, scale=0.02):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(M, K, generator=g) * scale).to(dtype)
+
+
+def _x(K, seed=1, dtype=torch.float16):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(K, generator=g).to(dtype)
+
+
+def _ulp(dtype):
+    return {torch.float16: 2.0 ** -10, torch.bfloat16: 2.0 ** -7, torch.float32: 2.0 ** -23}[dtype]
+
+
+def assert_close(y, yref, dtype, what=""):
+    y = np.asarray(y, np.float64).ravel()
+    yref = np.asarray(yref, np.float64).ravel()
+    rel = np.linalg.norm(y - yref) / max(np.linalg.norm(yref), 1e-30)
+    assert rel <= REL_TOL, f"{what}: rel err {rel:.3e}"
+    bound = 1e-3 * np.max(np.abs(yref)) + _ulp(dtype) * np.abs(yref) + 1e-30
+    worst = np.max(np.abs(y - yref) - bound)
+    assert worst <= 0, f"{what}: elementwise bound exceeded by {worst:.3e}"
+
+
+# ---------------------------------------------------------------------------
+# quantisation: bit-exact
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("qt", ["fp4", "nf4"])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,bs", [((128, 1024), 64), ((40, 2112), 64), ((3, 37), 64), ((257, 33), 128),
+                                      ((64, 1024), 256), ((16, 4096), 1024), ((8, 8192), 4096)])
+def test_quantize_4bit_bit_exact(orc, qt, dtype, shape, bs):
+    from quantizations_amd.core import quantize_4bit
+
+    W = _w(*shape, seed=shape[0] + 7 * shape[1] + bs + (qt == "nf4"), dtype=dtype)
+    packed, st = quantize_4bit(W.to(DEV), blocksize=bs, quant_type=qt, compress_statistics=True)
+    o = orc.quantize_4bit(W.float().numpy(), bs, qt, double_quant=True)
+    assert np.array_equal(packed.cpu().numpy().ravel(), o.packed)
+    assert float(st.offset) == float(o.offset) and st.offset.dtype == torch.float32
+    assert np.array_equal(st.absmax.cpu().numpy(), o.qabsmax)
+    assert np.array_equal(st.state2.absmax.cpu().numpy().view(np.uint32), o.absmax2.view(np.uint32))
+    p2, st_nodq = quantize_4bit(W.to(DEV), blocksize=bs, quant_type=qt, compress_statistics=False)
+    assert np.array_equal(p2.cpu().numpy().ravel(), o.packed)
+    assert np.array_equal(st_nodq.absmax.cpu().numpy().view(np.uint32), o.absmax_raw.view(np.uint32))
+
+
+def test_quantize_edge_values(orc):
+    from quantizations_amd.core import quantize_4bit
+
+    W = _w(4, 256, seed=5)
+    W[0, :64] = 0                   # all-zero block
+    W[1, 5] = float("nan")          # NaN ignored by absmax
+    W[2, 0] = 65504.0               # fp16 max
+    W[3, 64:] = -W[3, 64:].abs()    # negative-only blocks
+    for qt in ("fp4", "nf4"):
+        packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=False)
+        o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=False)
+        assert np.array_equal(packed.cpu().numpy().ravel(), o.packed)
+        assert np.array_equal(st.absmax.cpu().numpy().view(np.uint32), o.absmax_raw.view(np.uint32))
+
+
+def test_golden_vectors(oracle_vectors):
+    """Committed oracle vectors (tests/golden/oracle_vectors.npz)."""
+    from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
+
+    V = oracle_vectors
+    for key in sorted({k.rsplit("_", 1)[0] for k in V if k.endswith("_packed")}):
+        qt = key.split("_")[0]
+        W = torch.from_numpy(V[f"{key}_W"].view(np.float16))
+        x = torch.from_numpy(V[f"{key}_x"].view(np.float16))
+        packed, st = quantize_4bit(W.to(DEV), quant_type=qt)
+        assert np.array_equal(packed.cpu().numpy().ravel(), V[f"{key}_packed"]), key
+        assert np.array_equal(st.absmax.cpu().numpy(), V[f"{key}_qabsmax"]), key
+        assert float(st.offset) == float(V[f"{key}_offset"]), key
+        y = gemv_4bit(x.to(DEV).reshape(1, 1, -1), packed.t(), state=st)
+        assert_close(y.float().cpu(), V[f"{key}_y"], torch.float16, key)
+        wd = dequantize_4bit(packed, st).t().contiguous()
+        assert np.array_equal(wd.cpu().numpy().view(np.int16), V[f"{key}_wdeq16"]), key
+
+
+def test_absmax_mean_bit_exact(orc):
+    from quantizations_amd import _lib
+
+    for n in (1, 7, 1024, 1025, 262144, 917504, 3670016):
+        a = torch.rand(n, generator=torch.Generator().manual_seed(n)) * 0.05
+        ad = a.to(DEV)
+        off = torch.empty((), device=DEV)
+        ws = torch.empty(int(_lib.lib.qz_absmax_mean_workspace(n)), device=DEV, dtype=torch.float64)
+        _lib.check(_lib.lib.qz_absmax_mean(ad.data_ptr(), n, ws.data_ptr(), off.data_ptr(), 0), "mean")
+        assert float(off) == float(orc.absmax_mean(a.numpy())), n
+
+
+# ---------------------------------------------------------------------------
+# dequantisation: bit-exact
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("qt", ["fp4", "nf4"])
+@pytest.mark.parametrize("out_dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(128, 1024), (3, 37), (40, 2112)])
+def test_dequantize_4bit_bit_exact(orc, qt, out_dtype, shape):
+    from quantizations_amd.core import dequantize_4bit, quantize_4bit
+
+    W = _w(*shape, seed=11)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt)
+    wd = dequantize_4bit(packed, st, out_dtype=out_dtype)
+    assert wd.shape == (shape[1], shape[0])  # reference returns out.t() (core.py:634)
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt)
+    ref = torch.from_numpy(orc.dequantize(o)).to(out_dtype)
+    got = wd.t().contiguous().cpu()
+    assert torch.equal(got.view(torch.int16 if out_dtype != torch.float32 else torch.int32),
+                       ref.view(torch.int16 if out_dtype != torch.float32 else torch.int32))
+
+
+def test_fp4_dequant_negative_zero():
+    from quantizations_amd import kbkim_lib
+
+    packed = torch.tensor([0x88, 0x80, 0x08, 0x00] * 16, dtype=torch.uint8, device=DEV)
+    absmax = torch.ones(2, device=DEV)
+    out = torch.empty(128, dtype=torch.float16, device=DEV)
+    kbkim_lib.cdequantize_blockwise_fp16_fp4(0, packed.data_ptr(), absmax.data_ptr(), out.data_ptr(), 64, 128)
+    o = out.cpu()
+    assert torch.equal(o.view(torch.int16)[:8], torch.tensor([-32768, -32768, -32768, 0, 0, -32768, 0, 0],
+                                                             dtype=torch.int16))
+
+
+# ---------------------------------------------------------------------------
+# the five reference entry points (kbkim_lib), called as core.py calls them
+# ---------------------------------------------------------------------------
+
+
+def test_kbkim_lib_reference_call_sequence(orc):
+    from quantizations_amd import kbkim_lib
+
+    M, K = 512, 4096
+    W = _w(M, K, seed=21)
+    x = _x(K, seed=22).float()
+    n = M * K
+    Wd, xd = W.to(DEV), x.to(DEV)
+    absmax = torch.zeros(n // 64, device=DEV)
+    packed = torch.zeros((n // 2, 1), dtype=torch.uint8, device=DEV)
+    kbkim_lib.cquantize_blockwise_fp16_fp4(0, Wd.data_ptr(), absmax.data_ptr(), packed.data_ptr(), 64, n)  # core.py:552
+    o = orc.quantize_4bit(W.float().numpy(), 64, "fp4")
+    assert np.array_equal(packed.cpu().numpy().ravel(), o.packed)
+    # double quant exactly as core.py:563-565 (torch mean, subtract, quantize_blockwise)
+    offset = absmax.mean()
+    a = absmax - offset
+    code = torch.from_numpy(orc.create_dynamic_map()).to(DEV)
+    q = torch.zeros_like(a, dtype=torch.uint8)
+    a2 = torch.zeros(n // 64 // 256, device=DEV)
+    kbkim_lib.cquantize_blockwise_fp32(code.data_ptr(), a.data_ptr(), a2.data_ptr(), q.data_ptr(), 256, a.numel())
+    oq, oa2 = orc.quantize_blockwise_8bit(code.cpu().numpy(), a.cpu().numpy(), 256)
+    assert np.array_equal(q.cpu().numpy(), oq) and np.array_equal(a2.cpu().numpy(), oa2)
+    # decode: dequantize_blockwise + offset + GEMV (core.py:467-499)
+    am = torch.empty_like(a)
+    kbkim_lib.cdequantize_blockwise_fp32(code.data_ptr(), q.data_ptr(), a2.data_ptr(), am.data_ptr(), 256, q.numel())
+    am += offset
+    oam = orc.dequantize_blockwise_8bit(code.cpu().numpy(), oq, oa2, 256, float(offset))
+    assert np.array_equal(am.cpu().numpy(), oam)
+    lut = torch.from_numpy(orc.codebook("fp4")).to(DEV)
+    out = torch.empty(1, 1, M, device=DEV)
+    kbkim_lib.cgemm_4bit_inference_naive_fp32(M, 1, K, xd.data_ptr(), packed.data_ptr(), am.data_ptr(),
+                                              lut.data_ptr(), out.data_ptr(), M, (K + 1) // 2, M, 64)
+    yref = orc.gemv_4bit(x.numpy(), o.packed, oam, orc.codebook("fp4"), M, K, 64)
+    assert_close(out.cpu(), yref, torch.float32, "cgemm_4bit_inference_naive_fp32")
+    # prefill dequant (core.py:624)
+    wout = torch.empty(n, dtype=torch.float16, device=DEV)
+    kbkim_lib.cdequantize_blockwise_fp16_fp4(0, packed.data_ptr(), am.data_ptr(), wout.data_ptr(), 64, n)
+    ow = orc.dequantize_4bit(o.packed, oam, n, 64, "fp4").astype(np.float16)
+    assert np.array_equal(wout.cpu().numpy().view(np.int16), ow.view(np.int16))
+    with pytest.raises(TypeError):
+        kbkim_lib.cquantize_blockwise_fp32(1.5, 0, 0, 0, 256, 1)
+
+
+# ---------------------------------------------------------------------------
+# fused GEMV
+# ---------------------------------------------------------------------------
+
+GEMV_SHAPES = [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336), (1000, 2048), (37, 2112), (7, 96),
+               (130, 1024), (8, 8192), (3, 100), (5, 62)]
+
+
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("dq", [True, False])
+@pytest.mark.parametrize("shape", GEMV_SHAPES)
+def test_gemv_f16(orc, qt, dq, shape):
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+
+    M, K = shape
+    W = _w(M, K, seed=M + K)
+    x = _x(K, seed=K)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+    y = gemv_4bit(x.to(DEV).reshape(1, 1, K), packed.t(), state=st)
+    assert y.shape == (1, 1, M) and y.dtype == torch.float16
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=dq)
+    assert_close(y.float().cpu(), orc.gemv(x.float().numpy(), o), torch.float16, f"{qt} dq={dq} {shape}")
+
+
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(4096, 4096), (1024, 4096), (333, 2048), (7, 96), (5, 62)])
+def test_gemv_bf16_f32_activations(orc, qt, dtype, shape):
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+
+    M, K = shape
+    W = _w(M, K, seed=3 * M + K)
+    x = _x(K, seed=2 * K, dtype=dtype)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt)
+    y = gemv_4bit(x.to(DEV).reshape(1, K), packed.t(), state=st)
+    assert y.shape == (1, M) and y.dtype == dtype
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt)
+    assert_close(y.float().cpu(), orc.gemv(x.float().numpy(), o), dtype, f"{qt} {dtype} {shape}")
+
+
+def test_gemv_bias_and_large_activations(orc):
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+
+    M, K = 2048, 4096
+    W = _w(M, K, seed=77)
+    x = _x(K, seed=78) * 300  # large activations (fp16 range), fp32 path split hi/lo
+    bias = torch.randn(M, generator=torch.Generator().manual_seed(79))
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    o = orc.quantize_4bit(W.float().numpy(), 64, "nf4")
+    yref = orc.gemv(x.float().numpy(), o) + bias.numpy().astype(np.float64)
+    for dt in (torch.float16, torch.float32):
+        y = gemv_4bit(x.to(dt).to(DEV).reshape(1, 1, K), packed, state=st, bias=bias.to(dt).to(DEV))
+        yr = orc.gemv(x.to(dt).float().numpy(), o) + bias.to(dt).float().numpy()
+        assert_close(y.float().cpu(), yr, dt, f"bias {dt}")
+    del yref
+
+
+def test_gemv_deterministic_and_full_size_properties(orc):
+    """4096x4096 (the headline shape): repeat launches are bitwise identical and
+    y is linear in x (y(2x) == 2 y(x) exactly for fp32 accumulation of fp16 inputs)."""
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+
+    W = _w(4096, 4096, seed=99)
+    x = _x(4096, seed=98).to(DEV).reshape(1, 1, -1)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    y1 = gemv_4bit(x, packed, state=st)
+    y2 = gemv_4bit(x, packed, state=st)
+    assert torch.equal(y1, y2)
+    y3 = gemv_4bit(x.float() * 2, packed, state=st)
+    y4 = gemv_4bit(x.float(), packed, state=st)
+    assert torch.allclose(y3, 2 * y4, rtol=1e-5, atol=1e-6)
+    o = orc.quantize_4bit(W.float().numpy(), 64, "nf4")
+    assert_close(y4.cpu(), orc.gemv(x.float().cpu().numpy().ravel(), o), torch.float32, "4096 fp32")
+
+
+def test_gemv_row_shard_block_base(orc):
+    """A row shard addressed with block_base gives the same rows as the full layer."""
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+    from quantizations_amd.parallel import shard_rows
+
+    M, K = 96, 640
+    W = _w(M, K, seed=41)
+    x = _x(K, seed=42).to(DEV).reshape(1, K)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    full = gemv_4bit(x, packed, state=st)
+    for world in (2, 4):
+        for r in range(world):
+            sh = shard_rows(packed, st, r, world)
+            y = gemv_4bit(x, sh.packed, state=sh.state, block_base=sh.block_base)
+            assert torch.equal(y, full[:, sh.r0:sh.r1]), (world, r)
+
+
+# ---------------------------------------------------------------------------
+# fused prefill GEMM (MFMA)
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("dq", [True, False])
+@pytest.mark.parametrize("T,M,K", [(128, 128, 64), (200, 384, 1024), (17, 4096, 4096), (1024, 1024, 4096),
+                                   (64, 14336, 4096), (33, 4096, 14336)])
+def test_gemm_prefill(orc, qt, dq, T, M, K):
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    W = _w(M, K, seed=T + M)
+    g = torch.Generator().manual_seed(T)
+    X = torch.randn(T, K, generator=g).to(torch.float16)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+    Y = gemm_4bit(X.to(DEV), packed, st)
+    assert Y.shape == (T, M) and Y.dtype == torch.float16
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=dq)
+    Wd = torch.from_numpy(orc.dequantize(o)).double()
+    Yref = (X.double() @ Wd.t()).numpy()
+    assert_close(Y.float().cpu(), Yref, torch.float16, f"gemm {qt} dq={dq} {T}x{M}x{K}")
+
+
+def test_gemm_bias_and_batch_dims(orc):
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    T, M, K = 2 * 77, 640, 512
+    W = _w(M, K, seed=5)
+    X = torch.randn(2, 77, K, generator=torch.Generator().manual_seed(6)).to(torch.float16)
+    bias = torch.randn(M, generator=torch.Generator().manual_seed(7)).to(torch.float16)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    Y = gemm_4bit(X.to(DEV), packed, st, bias=bias.to(DEV))
+    o = orc.quantize_4bit(W.float().numpy(), 64, "nf4")
+    Wd = torch.from_numpy(orc.dequantize(o)).double()
+    Yref = (X.reshape(T, K).double() @ Wd.t() + bias.double()).numpy()
+    assert Y.shape == (2, 77, M)
+    assert_close(Y.reshape(T, M).float().cpu(), Yref, torch.float16, "gemm bias")
+
+
+# ---------------------------------------------------------------------------
+# module level: Linear4bit drop-in
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("qt", ["fp4", "nf4"])
+def test_linear4bit_decode_and_prefill(orc, qt):
+    import quantizations_amd as qa
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(1024, 768, bias=True).half()
+    m = qa.Linear4bit(1024, 768, bias=True, compute_dtype=torch.float32, quant_type=qt)
+    m.weight = qa.Params4bit(lin.weight.data.clone(), requires_grad=False, quant_type=qt, module=m)
+    m.bias = torch.nn.Parameter(lin.bias.data.clone(), requires_grad=False)
+    m = m.to(DEV)
+    assert m.weight.bnb_quantized and m.quant_state is m.weight.quant_state
+    o = orc.quantize_4bit(lin.weight.data.float().numpy(), 64, qt)
+    Wd = torch.from_numpy(orc.dequantize(o)).double()
+    x1 = torch.randn(1, 1, 1024).half()
+    y1 = m(x1.to(DEV))
+    assert y1.dtype == torch.float16 and y1.shape == (1, 1, 768)
+    assert_close(y1.float().cpu(), (x1.double().reshape(1, -1) @ Wd.t() + lin.bias.double()).numpy(),
+                 torch.float16, "decode")
+    x2 = torch.randn(2, 9, 1024).half()
+    y2 = m(x2.to(DEV))
+    assert y2.shape == (2, 9, 768)
+    assert_close(y2.float().cpu().reshape(18, -1),
+                 (x2.double().reshape(18, -1) @ Wd.t() + lin.bias.double()).numpy(), torch.float16, "prefill")
+
+
+def test_linear4bit_hip_graph_capture(orc):
+    """The decode path launches on torch's current stream and is capturable."""
+    import quantizations_amd as qa
+
+    m = qa.Linear4bit(4096, 4096, quant_type="nf4").half()
+    m = m.to(DEV)
+    x = torch.randn(1, 1, 4096, device=DEV, dtype=torch.float16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            m(x)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = m(x)
+    x.copy_(torch.randn_like(x))
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, m(x))
+
+
+def test_tiny_llama_with_linear4bit(orc):
+    """replace_with_bnb_linear on a small LlamaForCausalLM: logits match the same
+    model with the dequantised weights in a plain fp32 nn.Linear."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import replace_with_bnb_linear
+    import quantizations_amd as qa
+
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=512)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, quant_type="nf4")
+    ids = torch.randint(0, 512, (1, 12), device=DEV)
+    with torch.no_grad():
+        out = model(input_ids=ids).logits.float()
+        # reference: same model, each Linear4bit replaced by fp32 linear on its dequantised weight
+        ref = LlamaForCausalLM(cfg).to(DEV).eval()
+        ref.load_state_dict({k: v for k, v in model.state_dict().items() if "weight" in k and v.dtype != torch.uint8},
+                            strict=False)
+        for name, mod in model.named_modules():
+            if isinstance(mod, qa.Linear4bit):
+                tgt = ref.get_submodule(name)
+                tgt.weight.data.copy_(mod.dequantize().float())
+        out_ref = ref(input_ids=ids).logits.float()
+    rel = (out - out_ref).norm() / out_ref.norm()
+    assert rel < 5e-3, rel

@@ -1,0 +1,93 @@
+"""Host-side mirror of the reference interface (no GPU needed)."""
+import inspect
+
+import numpy as np
+import pytest
+import torch
+
+import quantizations_amd as qa
+from quantizations_amd import core, modules
+
+
+def test_linear4bit_signature_matches_reference():
+    # reference modules.py:86-96
+    params = list(inspect.signature(modules.Linear4bit.__init__).parameters)
+    assert params == ["self", "input_features", "output_features", "bias", "compute_dtype", "compress_statistics",
+                      "quant_type", "quant_storage", "device"]
+    p = inspect.signature(modules.Linear4bit.__init__).parameters
+    assert p["bias"].default is False and p["quant_type"].default == "fp4" and p["compress_statistics"].default
+
+
+def test_params4bit_signature_and_kwargs():
+    params = list(inspect.signature(core.Params4bit.__new__).parameters)
+    assert params[:9] == ["cls", "data", "requires_grad", "quant_state", "blocksize", "quant_type", "quant_storage",
+                          "module", "bnb_quantized"]
+    # transformers: Params4bit(value, requires_grad=False, **old.__dict__) must not fail on extra keys
+    p = core.Params4bit(torch.zeros(4, 4), requires_grad=False, quant_type="nf4", _is_hf_initialized=True)
+    assert p.quant_type == "nf4" and not p.bnb_quantized
+
+
+def test_codebooks(ref_tables):
+    assert np.array_equal(core.get_4bit_type("fp4", device="cpu").numpy().view(np.uint32),
+                          ref_tables["fp4_lut"].view(np.uint32))
+    nf4 = core.get_4bit_type("nf4", device="cpu")
+    assert nf4[7] == 0 and nf4[0] == -1 and nf4[15] == 1
+    with pytest.raises(NotImplementedError):
+        core.get_4bit_type("int4", device="cpu")
+
+
+def test_dynamic_map_matches_reference(ref_tables):
+    assert np.array_equal(core.create_dynamic_map().numpy().view(np.uint32), ref_tables["dynamic_map"].view(np.uint32))
+
+
+def test_quantize_requires_gpu_like_reference():
+    with pytest.raises(NotImplementedError):
+        core.quantize_4bit(torch.zeros(64, dtype=torch.float16))
+    with pytest.raises(NotImplementedError):
+        core.quantize_4bit(torch.zeros(64, dtype=torch.float16, device="meta"), quant_type="int4")
+
+
+def test_gemv_argument_errors_like_reference():
+    st = core.QuantState(absmax=torch.zeros(4), shape=torch.Size([8, 32]), blocksize=64, quant_type="fp4")
+    with pytest.raises(ValueError, match="state cannot None"):
+        core.gemv_4bit(torch.zeros(1, 1, 32), torch.zeros(1), state=None)
+    with pytest.raises(ValueError, match="Dimensions of A are invalid"):
+        core.gemv_4bit(torch.zeros(2, 1, 32), torch.zeros(1), state=st)
+    with pytest.raises(ValueError):
+        core.dequantize_4bit(torch.zeros(1), st, blocksize=96)
+
+
+def test_quant_state_dict_roundtrip():
+    st2 = core.QuantState(absmax=torch.rand(2), blocksize=256, code=core.create_dynamic_map(), dtype=torch.float32)
+    st = core.QuantState(absmax=torch.randint(0, 255, (300,), dtype=torch.uint8), shape=torch.Size([60, 320]),
+                         code=core.get_4bit_type("nf4", device="cpu"), blocksize=64, quant_type="nf4",
+                         dtype=torch.float16, offset=torch.tensor(0.25), state2=st2)
+    d = st.as_dict()
+    assert set(k for k in d) <= set(core.QuantState.valid_qs_keys)
+    back = core.QuantState.from_dict(d, device="cpu")
+    assert back.nested and back.quant_type == "nf4" and back.shape == st.shape and back.dtype == torch.float16
+    assert torch.equal(back.absmax, st.absmax) and torch.equal(back.state2.absmax, st2.absmax)
+    assert float(back.offset) == 0.25
+
+
+def test_module_needs_quantisation_before_forward():
+    m = qa.Linear4bit(32, 8, quant_type="nf4")
+    with pytest.raises(RuntimeError, match="not quantised"):
+        m(torch.zeros(1, 1, 32, dtype=torch.float16))
+
+
+def test_replace_with_bnb_linear_skips_lm_head_on_meta():
+    from quantizations_amd.integration import replace_with_bnb_linear
+
+    class Tiny(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.proj = torch.nn.Linear(64, 64)
+            self.lm_head = torch.nn.Linear(64, 10)
+
+    with torch.device("meta"):
+        t = Tiny()
+    # meta weights never reach .to(cuda) -> not quantised, but the module types are swapped
+    replace_with_bnb_linear(t, quant_type="nf4", device="meta")
+    assert isinstance(t.proj, qa.Linear4bit) and not isinstance(t.lm_head, qa.Linear4bit)
+    assert t.proj.weight.quant_type == "nf4" and t.proj.weight.compress_statistics

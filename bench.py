@@ -100,6 +100,56 @@ def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: in
 
 
 @torch.inference_mode()
+def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int):
+    """Same workload as decode_bench, with the decode step captured once into a HIP
+    graph (StaticCache, static token/position buffers; the graph contains the
+    whole forward, the argmax and the feedback of the token into the next
+    step).  One replay = one generated token."""
+    from transformers.cache_utils import StaticCache
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    ids = torch.randint(0, cfg.vocab_size, (1, prompt_len), generator=g).to(dev)
+    cache = StaticCache(config=cfg, max_cache_len=prompt_len + warmup + steps + 8)
+    out = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(prompt_len, device=dev),
+                use_cache=True)
+    tok = out.logits[:, -1:].argmax(-1)
+    pos = torch.tensor([prompt_len], device=dev, dtype=torch.long)
+    hist = torch.zeros((1, prompt_len + warmup + steps + 8), device=dev, dtype=torch.long)
+
+    def step():
+        lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos.view(1, 1),
+                   use_cache=True).logits
+        nxt = lo[:, -1:].argmax(-1)
+        hist.index_copy_(1, pos, nxt.view(1, 1))
+        tok.copy_(nxt)
+        pos.add_(1)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step()
+    for _ in range(warmup):
+        graph.replay()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    return dt, hist
+
+
+@torch.inference_mode()
 def gemv_roofline(copies: int = 64, iters: int = 400):
     """Per-launch duration of the 4096x4096 NF4+DQ fused GEMV (rotating weights)."""
     from quantizations_amd import _lib
@@ -126,20 +176,35 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
     for i in range(2 * copies):
         launch(i)
     torch.cuda.synchronize()
+
+    def blocked(fn_body):
+        # Park the stream behind a ~50 ms spin kernel so the host enqueues every
+        # launch (and event) before the GPU reaches them: the events then time
+        # GPU execution, not Python/ctypes submission latency.
+        torch.cuda._sleep(100_000_000)
+        fn_body()
+        torch.cuda.synchronize()
+
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
-    for i in range(iters):
-        ev[i][0].record()
-        launch(i)
-        ev[i][1].record()
-    torch.cuda.synchronize()
+
+    def per_launch():
+        for i in range(iters):
+            ev[i][0].record()
+            launch(i)
+            ev[i][1].record()
+
+    blocked(per_launch)
     us = [a.elapsed_time(b) * 1e3 for a, b in ev]
-    # back-to-back throughput (includes launch gaps) for reference
+    # back-to-back stream throughput (kernel + inter-kernel gap), also host-decoupled
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(iters):
-        launch(i)
-    e1.record()
-    torch.cuda.synchronize()
+
+    def b2b():
+        e0.record()
+        for i in range(iters):
+            launch(i)
+        e1.record()
+
+    blocked(b2b)
     b2b_us = e0.elapsed_time(e1) * 1e3 / iters
     return statistics.mean(us), statistics.median(us), b2b_us
 
@@ -149,7 +214,8 @@ def cpu_baseline(target_s: float = 12.0):
 
     import oracle
 
-    cores = len(os.sched_getaffinity(0))
+    # the GPU box exposes the whole machine's CPUs; its share is OMP_NUM_THREADS (16)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(cores)
     g = torch.Generator().manual_seed(0)
     W = (torch.randn(4096, 4096, generator=g) * 0.02).to(torch.float16)
@@ -180,7 +246,9 @@ def main():
     ap.add_argument("--prompt", type=int, default=32)
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the decode step")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--gemv-only", action="store_true", help="only the 4096x4096 roofline microbench (profiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -192,6 +260,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.gemv_only:
+        mean_us, med_us, b2b_us = gemv_roofline()
+        print(json.dumps({"gemv_4096_us_mean": mean_us, "gemv_4096_us_median": med_us, "back_to_back_us": b2b_us,
+                          "achieved_GBs": GEMV_BYTES_4096 / (mean_us * 1e-6) / 1e9}), flush=True)
+        return
+
     t_build = time.perf_counter()
     model, cfg = build_model(args.layers, seed=0)
     if world > 1:
@@ -201,7 +275,16 @@ def main():
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 
-    dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world)
+    mode = "eager"
+    if not args.eager:
+        try:
+            dt, toks = decode_bench_graph(model, cfg, args.steps, args.warmup, args.prompt, world)
+            mode = "hipgraph"
+        except Exception as e:  # capture unsupported by this transformers build -> eager
+            log(f"[rank {rank}] graph decode failed ({type(e).__name__}: {e}); falling back to eager")
+            torch.cuda.synchronize()
+    if mode == "eager":
+        dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world)
     t = torch.tensor([dt], device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -237,7 +320,7 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
-                       "prompt_len": args.prompt, "batch": 1,
+                       "prompt_len": args.prompt, "batch": 1, "decode": mode,
                        "parallelism": "single" if world == 1 else f"rowsplit-tp{world}-allgather"},
             "roofline": roof, "cpu_baseline": cpu,
         }

@@ -97,9 +97,21 @@ template <int DT> __device__ __forceinline__ float load_f32(const void *p, long 
   }
 }
 
+// fp32 -> 2 x fp16, round-to-nearest-even.  Measured on gfx950 (ROCm 7.2):
+// the packed v_cvt_pk_f16_f32 rounds exact ties to even, while the scalar
+// v_cvt_f16_f32 that __float2half_rn can lower to rounded the tie 0x3c8d1000
+// UP (0x2469 instead of 0x2468; tests/test_gpu_rounding.py).  Every fp16 store
+// that must be bit-exact goes through the packed instruction.
+__device__ __forceinline__ uint32_t cvt_pk_f16_rne(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ __forceinline__ uint16_t f32_to_f16_bits(float v) { return (uint16_t)cvt_pk_f16_rne(v, 0.0f); }
+
 template <int DT> __device__ __forceinline__ void store_f32(void *p, long long i, float v) {
   if constexpr (DT == QZ_DT_F16) {
-    reinterpret_cast<__half *>(p)[i] = __float2half_rn(v);
+    reinterpret_cast<uint16_t *>(p)[i] = f32_to_f16_bits(v);
   } else if constexpr (DT == QZ_DT_BF16) {
     reinterpret_cast<__hip_bfloat16 *>(p)[i] = __float2bfloat16(v);
   } else {

@@ -53,15 +53,13 @@ __global__ __launch_bounds__(256) void k_dequantize_4bit(const unsigned char *__
       uint32_t pk[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        uint16_t a, b;
         if constexpr (ODT == QZ_DT_F16) {
-          a = __half_as_ushort(__float2half_rn(v[2 * j]));
-          b = __half_as_ushort(__float2half_rn(v[2 * j + 1]));
+          pk[j] = cvt_pk_f16_rne(v[2 * j], v[2 * j + 1]);
         } else {
-          a = __bfloat16_as_ushort(__float2bfloat16(v[2 * j]));
-          b = __bfloat16_as_ushort(__float2bfloat16(v[2 * j + 1]));
+          const uint16_t a = __bfloat16_as_ushort(__float2bfloat16(v[2 * j]));
+          const uint16_t b = __bfloat16_as_ushort(__float2bfloat16(v[2 * j + 1]));
+          pk[j] = (uint32_t)a | ((uint32_t)b << 16);
         }
-        pk[j] = (uint32_t)a | ((uint32_t)b << 16);
       }
       uint4 *o = reinterpret_cast<uint4 *>(reinterpret_cast<uint16_t *>(out) + e0);
       o[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void k_gemm_4bit_f16(GemmParams p) {
       for (int r = 0; r < 4; ++r) {
         const int t = t0 + 64 * wt + 16 * i + 4 * fk + r;
         if (t < p.T)
-          reinterpret_cast<__half *>(p.Y)[(size_t)t * p.ldy + m] = __float2half_rn(acc[i][j][r] + bv);
+          reinterpret_cast<uint16_t *>(p.Y)[(size_t)t * p.ldy + m] = f32_to_f16_bits(acc[i][j][r] + bv);
       }
   }
 }

@@ -38,7 +38,7 @@
 
 namespace qz {
 
-enum { kModeFP4 = 0, kModeLUT16 = 1 };
+enum { kModeFP4 = 0, kModeLUT16 = 1, kModeRaw = 2 /* benchmark-only: no decode */ };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -92,63 +92,50 @@ __device__ __forceinline__ void decode_lut16(uint32_t w, const uint32_t (&t)[8],
   P[3] = perm(hl, ll, 0x07030602u);
 }
 
-// x slice of one lane for one step: 32 elements as 16 half2 "hi" (and "lo"
-// for fp32/bf16 activations), arranged in the pair order of MODE.
+// x slice of one lane for one step: 32 activations, loaded raw (so that the
+// loads retire in issue order without forcing early waits) and turned into
+// 16 half2 "hi" (+ "lo" for fp32/bf16 activations) in the pair order of MODE
+// only at compute time.
 template <int MODE, int DT> struct XSlice {
   static constexpr bool kSplit = DT != QZ_DT_F16;
-  uint32_t hi[16];
-  uint32_t lo[kSplit ? 16 : 1];
+  static constexpr int kWords = DT == QZ_DT_F32 ? 32 : 16;  // raw dwords per lane
+  uint32_t raw[kWords];
 
-  __device__ __forceinline__ void zero() {
+  __device__ __forceinline__ void load(const void *x, long long e0) {
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(x) +
+                                                     e0 * (DT == QZ_DT_F32 ? 4 : 2));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) hi[i] = 0;
-    if constexpr (kSplit) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) lo[i] = 0;
+    for (int i = 0; i < kWords / 4; ++i) {
+      const u32x4 v = p[i];
+      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
     }
   }
 
-  __device__ __forceinline__ void load(const void *x, long long e0) {
+  // hi/lo half2 operands, pair order of MODE
+  __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1]) const {
     if constexpr (DT == QZ_DT_F16) {
-      const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(x) + e0);
-      uint32_t n[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 v = p[i];
-        n[4 * i] = v.x; n[4 * i + 1] = v.y; n[4 * i + 2] = v.z; n[4 * i + 3] = v.w;
-      }
       if constexpr (MODE == kModeFP4) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) hi[i] = n[i];
+        for (int i = 0; i < 16; ++i) hi[i] = raw[i];
       } else {
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // per 8 elements: (x0,x2),(x4,x6),(x1,x3),(x5,x7)
-          hi[4 * d + 0] = perm(n[4 * d + 1], n[4 * d + 0], 0x05040100u);
-          hi[4 * d + 1] = perm(n[4 * d + 3], n[4 * d + 2], 0x05040100u);
-          hi[4 * d + 2] = perm(n[4 * d + 1], n[4 * d + 0], 0x07060302u);
-          hi[4 * d + 3] = perm(n[4 * d + 3], n[4 * d + 2], 0x07060302u);
+          hi[4 * d + 0] = perm(raw[4 * d + 1], raw[4 * d + 0], 0x05040100u);
+          hi[4 * d + 1] = perm(raw[4 * d + 3], raw[4 * d + 2], 0x05040100u);
+          hi[4 * d + 2] = perm(raw[4 * d + 1], raw[4 * d + 0], 0x07060302u);
+          hi[4 * d + 3] = perm(raw[4 * d + 3], raw[4 * d + 2], 0x07060302u);
         }
       }
     } else {
       float f[32];
       if constexpr (DT == QZ_DT_F32) {
-        const float4 *p = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(x) + e0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float4 v = p[i];
-          f[4 * i] = v.x; f[4 * i + 1] = v.y; f[4 * i + 2] = v.z; f[4 * i + 3] = v.w;
-        }
+        for (int i = 0; i < 32; ++i) f[i] = __uint_as_float(raw[i]);
       } else {
-        const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(x) + e0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint4 v = p[i];
-          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            f[8 * i + 2 * j] = __uint_as_float(u[j] << 16);
-            f[8 * i + 2 * j + 1] = __uint_as_float(u[j] & 0xFFFF0000u);
-          }
+        for (int i = 0; i < 16; ++i) {
+          f[2 * i] = __uint_as_float(raw[i] << 16);
+          f[2 * i + 1] = __uint_as_float(raw[i] & 0xFFFF0000u);
         }
       }
 #pragma unroll
@@ -161,8 +148,8 @@ template <int MODE, int DT> struct XSlice {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float fa = f[8 * d + a[j]], fb = f[8 * d + b[j]];
           // hi = rtz(f) (never overflows to inf below 65536), lo = rtz(f - hi); f - hi is exact
+          const float fa = f[8 * d + a[j]], fb = f[8 * d + b[j]];
           const auto h = __builtin_amdgcn_cvt_pkrtz(fa, fb);
           const float ra = fa - (float)h.x, rb = fb - (float)h.y;
           hi[4 * d + j] = __builtin_bit_cast(uint32_t, h);
@@ -174,75 +161,94 @@ template <int MODE, int DT> struct XSlice {
 };
 
 // dot of one lane's 16-byte weight chunk (32 codes) with its x slice
-template <int MODE, int DT>
-__device__ __forceinline__ float chunk_dot(const u32x4 &wv, const XSlice<MODE, DT> &xs, const uint32_t (&t)[8]) {
+template <int MODE, bool SPLIT>
+__device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)[16],
+                                           const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t (&t)[8]) {
   const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
   float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     uint32_t P[4];
-    if constexpr (MODE == kModeFP4) decode_fp4(w[d], t[0], t[1], P);
-    else decode_lut16(w[d], t, P);
+    if constexpr (MODE == kModeFP4) {
+      decode_fp4(w[d], t[0], t[1], P);
+    } else if constexpr (MODE == kModeLUT16) {
+      decode_lut16(w[d], t, P);
+    } else {
+      P[0] = w[d]; P[1] = w[d] ^ 1u; P[2] = w[d] ^ 2u; P[3] = w[d] ^ 3u;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (j & 1) s1 = dot2(P[j], xs.hi[4 * d + j], s1);
-      else s0 = dot2(P[j], xs.hi[4 * d + j], s0);
-      if constexpr (XSlice<MODE, DT>::kSplit) {
-        if (j & 1) s1 = dot2(P[j], xs.lo[4 * d + j], s1);
-        else s0 = dot2(P[j], xs.lo[4 * d + j], s0);
+      if (j & 1) s1 = dot2(P[j], hi[4 * d + j], s1);
+      else s0 = dot2(P[j], hi[4 * d + j], s0);
+      if constexpr (SPLIT) {
+        if (j & 1) s1 = dot2(P[j], lo[4 * d + j], s1);
+        else s0 = dot2(P[j], lo[4 * d + j], s0);
       }
     }
   }
   return s0 + s1;
 }
 
+// Sum over the 64 lanes with DPP row ops (no LDS round trips): quad swaps,
+// half-row and row mirrors reduce each 16-lane row, then the four row sums
+// are read back as scalars.  The result is wave-uniform.
+template <int CTRL> __device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+  v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);  // row_half_mirror
+  v = dpp_add<0x140>(v);  // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
 }
 
-// One step's worth of loads for R rows (issued together, consumed later).
+// One step's worth of loads for R rows.  Branch-free: out-of-range rows and
+// the inactive tail lanes of the last step read a clamped in-bounds address
+// and are zeroed at compute time, so the compiler issues every load up front
+// (no exec-masked regions, no lazily re-read kernel arguments).
 template <int MODE, bool DQ, int DT, int R> struct StepLoads {
   u32x4 wv[R];
   uint32_t q[R];    // DQ: 8-bit scale code
   float a[R];       // DQ: absmax2 entry; else: fp32 absmax
   XSlice<MODE, DT> xs;
+  bool on;
 
   __device__ __forceinline__ void issue(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
-    const int boff = (s << 10) + (lane << 4);
-    const bool on = boff < row_bytes;
+    const int boff_raw = (s << 10) + (lane << 4);
+    on = boff_raw < row_bytes;
+    const int boff = on ? boff_raw : 0;
+    xs.load(p.x, 2LL * boff);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int row = row0 + r;
-      const bool ok = on && row < p.M;
-      const long long e = (long long)row * p.K + 2 * boff;
-      const long long b = p.block_base + (e >> p.bs_log2);
-      if (ok) {
-        wv[r] = __builtin_nontemporal_load(
-            reinterpret_cast<const u32x4 *>(p.B + (size_t)row * (size_t)row_bytes + (size_t)boff));
-        if constexpr (DQ) {
-          q[r] = p.sc.qabsmax[b];
-          a[r] = p.sc.absmax2[b >> p.bs2_log2];
-        } else {
-          a[r] = p.sc.absmax[b];
-        }
+      const int row = min(row0 + r, p.M - 1);
+      wv[r] = __builtin_nontemporal_load(
+          reinterpret_cast<const u32x4 *>(p.B + (size_t)row * (size_t)row_bytes + (size_t)boff));
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int row = min(row0 + r, p.M - 1);
+      const long long b = p.block_base + (((long long)row * p.K + 2 * boff) >> p.bs_log2);
+      if constexpr (DQ) {
+        q[r] = p.sc.qabsmax[b];
+        a[r] = p.sc.absmax2[b >> p.bs2_log2];
       } else {
-        wv[r] = u32x4{0u, 0u, 0u, 0u};
-        q[r] = 0;
-        a[r] = 0.0f;
+        a[r] = p.sc.absmax[b];
       }
     }
-    if (on) xs.load(p.x, 2LL * boff);
-    else xs.zero();
   }
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK>
-__global__ __launch_bounds__(256) void k_gemv_4bit(GemvParams p) {
-  constexpr int RG = 4 / WK;
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
+  constexpr int RG = NW / WK;
+  constexpr bool kSplit = DT != QZ_DT_F16;
   __shared__ float s_code2[DQ ? 256 : 1];
-  __shared__ float s_part[4][R];
+  __shared__ float s_part[NW][R];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -252,15 +258,20 @@ __global__ __launch_bounds__(256) void k_gemv_4bit(GemvParams p) {
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
 
-  // issue the first step's HBM loads before anything that waits
+  // 1. the double-quant code table load goes out first (it gates the barrier)
+  float c2 = 0.0f, offset = 0.0f;
+  if constexpr (DQ) {
+    if (NW * 64 == 256 || threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x & 255];
+    offset = *p.sc.offset;
+  }
+  // 2. this wave's first step of HBM traffic
   StepLoads<MODE, DQ, DT, R> cur;
   int s = wk;
-  if (s < nsteps) cur.issue(p, row0, s, lane, row_bytes);
-
-  float offset = 0.0f;
+  cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
+  const bool have = s < nsteps;
+  // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
-    s_code2[threadIdx.x] = p.sc.code2[threadIdx.x];
-    offset = *p.sc.offset;
+    if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
     __syncthreads();
   }
 
@@ -283,18 +294,24 @@ __global__ __launch_bounds__(256) void k_gemv_4bit(GemvParams p) {
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 
-  for (; s < nsteps; s += WK) {
-    StepLoads<MODE, DQ, DT, R> nxt;
-    const bool more = s + WK < nsteps;
-    if (more) nxt.issue(p, row0, s + WK, lane, row_bytes);
+  if (have) {
+    for (;; s += WK) {
+      StepLoads<MODE, DQ, DT, R> nxt;
+      const bool more = s + WK < nsteps;
+      if (more) nxt.issue(p, row0, s + WK, lane, row_bytes);
+      uint32_t hi[16], lo[kSplit ? 16 : 1];
+      cur.xs.prepare(hi, lo);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float am;
-      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cur.q[r]], cur.a[r]), offset);
-      else am = cur.a[r];
-      acc[r] = fmaf(chunk_dot<MODE, DT>(cur.wv[r], cur.xs, t), am, acc[r]);
+      for (int r = 0; r < R; ++r) {
+        float am;
+        if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cur.q[r]], cur.a[r]), offset);
+        else am = cur.a[r];
+        am = cur.on ? am : 0.0f;
+        acc[r] = fmaf(chunk_dot<MODE, kSplit>(cur.wv[r], hi, lo, t), am, acc[r]);
+      }
+      if (!more) break;
+      cur = nxt;
     }
-    if (more) cur = nxt;
   }
 
 #pragma unroll

@@ -33,8 +33,13 @@ def _ulp(dtype):
 
 
 def assert_close(y, yref, dtype, what=""):
+    """1e-3 relative (north_star) on the fp32-accumulated result.  A bf16 output
+    cannot carry 1e-3 (its own rounding is up to 2^-9), so for bf16 the
+    reference is rounded to bf16 first and the bar applies to the difference."""
     y = np.asarray(y, np.float64).ravel()
     yref = np.asarray(yref, np.float64).ravel()
+    if dtype == torch.bfloat16:
+        yref = torch.from_numpy(yref).to(torch.bfloat16).double().numpy()
     rel = np.linalg.norm(y - yref) / max(np.linalg.norm(yref), 1e-30)
     assert rel <= REL_TOL, f"{what}: rel err {rel:.3e}"
     bound = 1e-3 * np.max(np.abs(yref)) + _ulp(dtype) * np.abs(yref) + 1e-30
@@ -96,8 +101,10 @@ def test_golden_vectors(oracle_vectors):
         assert float(st.offset) == float(V[f"{key}_offset"]), key
         y = gemv_4bit(x.to(DEV).reshape(1, 1, -1), packed.t(), state=st)
         assert_close(y.float().cpu(), V[f"{key}_y"], torch.float16, key)
-        wd = dequantize_4bit(packed, st).t().contiguous()
-        assert np.array_equal(wd.cpu().numpy().view(np.int16), V[f"{key}_wdeq16"]), key
+        assert np.array_equal(st.state2.absmax.cpu().numpy(), V[f"{key}_absmax2"]), key
+        wd = dequantize_4bit(packed, st).t().contiguous().cpu().numpy().view(np.int16)
+        bad = np.argwhere(wd != V[f"{key}_wdeq16"])
+        assert bad.size == 0, (key, len(bad), bad[:5].tolist(), wd[tuple(bad[0])], V[f"{key}_wdeq16"][tuple(bad[0])])
 
 
 def test_absmax_mean_bit_exact(orc):
@@ -336,7 +343,7 @@ def test_linear4bit_decode_and_prefill(orc, qt):
     import quantizations_amd as qa
 
     torch.manual_seed(0)
-    lin = torch.nn.Linear(1024, 768, bias=True).half()
+    lin = torch.nn.Linear(1024, 768, bias=True).half().requires_grad_(False)
     m = qa.Linear4bit(1024, 768, bias=True, compute_dtype=torch.float32, quant_type=qt)
     m.weight = qa.Params4bit(lin.weight.data.clone(), requires_grad=False, quant_type=qt, module=m)
     m.bias = torch.nn.Parameter(lin.bias.data.clone(), requires_grad=False)
@@ -347,13 +354,13 @@ def test_linear4bit_decode_and_prefill(orc, qt):
     x1 = torch.randn(1, 1, 1024).half()
     y1 = m(x1.to(DEV))
     assert y1.dtype == torch.float16 and y1.shape == (1, 1, 768)
-    assert_close(y1.float().cpu(), (x1.double().reshape(1, -1) @ Wd.t() + lin.bias.double()).numpy(),
+    assert_close(y1.float().cpu(), (x1.double().reshape(1, -1) @ Wd.t() + lin.bias.detach().double()).numpy(),
                  torch.float16, "decode")
     x2 = torch.randn(2, 9, 1024).half()
     y2 = m(x2.to(DEV))
     assert y2.shape == (2, 9, 768)
     assert_close(y2.float().cpu().reshape(18, -1),
-                 (x2.double().reshape(18, -1) @ Wd.t() + lin.bias.double()).numpy(), torch.float16, "prefill")
+                 (x2.double().reshape(18, -1) @ Wd.t() + lin.bias.detach().double()).numpy(), torch.float16, "prefill")
 
 
 def test_linear4bit_hip_graph_capture(orc):

@@ -65,6 +65,48 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, a), __builtin_bit_cast(h2_t, b), c, false);
 }
 
+// Kernel arguments are read ONCE at entry and laundered through an empty asm:
+// the compiler then keeps them in SGPRs instead of re-fetching them from the
+// kernarg segment at each use (every re-fetch is a serialized scalar-cache miss
+// on the critical path of a ~µs kernel).
+template <typename T> __device__ __forceinline__ T keep_s(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+template <typename T> __device__ __forceinline__ T *keep_sp(T *v) {
+  // launder as a GLOBAL (address space 1) pointer so that loads through the
+  // result are still selected as global_load (a generic pointer would become
+  // flat_load, which drains both vmcnt and lgkmcnt at every wait)
+  typedef __attribute__((address_space(1))) T *gptr;
+  gptr g = (gptr)v;
+  asm volatile("" : "+s"(g));
+  return (T *)g;
+}
+
+__device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
+  GemvParams p;
+  p.B = keep_sp(in.B);
+  p.x = keep_sp(in.x);
+  p.sc.absmax = keep_sp(in.sc.absmax);
+  p.sc.qabsmax = keep_sp(in.sc.qabsmax);
+  p.sc.absmax2 = keep_sp(in.sc.absmax2);
+  p.sc.code2 = keep_sp(in.sc.code2);
+  p.sc.offset = keep_sp(in.sc.offset);
+  p.sc.bs2 = keep_s(in.sc.bs2);
+  p.bias = keep_sp(in.bias);
+  p.y = keep_sp(in.y);
+  p.lut = keep_sp(in.lut);
+  p.block_base = keep_s(in.block_base);
+  p.M = keep_s(in.M);
+  p.K = keep_s(in.K);
+  p.bs_log2 = keep_s(in.bs_log2);
+  p.bs2_log2 = keep_s(in.bs2_log2);
+  p.out_scale = keep_s(in.out_scale);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
+  return p;
+}
+
 // FP4: 8 nibbles -> 4 half2 in natural order P[j] = (e_2j, e_2j+1), values x12.
 __device__ __forceinline__ void decode_fp4(uint32_t w, uint32_t t0, uint32_t t1, uint32_t (&P)[4]) {
   const uint32_t hh = perm(t1, t0, (w >> 4) & 0x07070707u) | (w & 0x80808080u);
@@ -104,6 +146,15 @@ template <int MODE, int DT> struct XSlice {
   __device__ __forceinline__ void load(const void *x, long long e0) {
     const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(x) +
                                                      e0 * (DT == QZ_DT_F32 ? 4 : 2));
+#pragma unroll
+    for (int i = 0; i < kWords / 4; ++i) {
+      const u32x4 v = p[i];
+      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+    }
+  }
+
+  __device__ __forceinline__ void load_lds(const unsigned char *lds_x, int e0) {
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(lds_x + e0 * (DT == QZ_DT_F32 ? 4 : 2));
 #pragma unroll
     for (int i = 0; i < kWords / 4; ++i) {
       const u32x4 v = p[i];
@@ -211,29 +262,36 @@ __device__ __forceinline__ float wave_sum(float v) {
 // the inactive tail lanes of the last step read a clamped in-bounds address
 // and are zeroed at compute time, so the compiler issues every load up front
 // (no exec-masked regions, no lazily re-read kernel arguments).
-template <int MODE, bool DQ, int DT, int R> struct StepLoads {
+template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoads {
   u32x4 wv[R];
   uint32_t q[R];    // DQ: 8-bit scale code
   float a[R];       // DQ: absmax2 entry; else: fp32 absmax
   XSlice<MODE, DT> xs;
+  int xb;  // first activation index of this lane's chunk
   bool on;
 
   __device__ __forceinline__ void issue(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
     const int boff_raw = (s << 10) + (lane << 4);
     on = boff_raw < row_bytes;
     const int boff = on ? boff_raw : 0;
-    xs.load(p.x, 2LL * boff);
+    xb = 2 * boff;
+    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2LL * boff);
+    if constexpr (ABL & 2) {
+#pragma unroll
+      for (int i = 0; i < XSlice<MODE, DT>::kWords; ++i) xs.raw[i] = 0x3C003C00u ^ (uint32_t)boff;
+    }
+    // per row: weights then that row's scale, so row r can be consumed while
+    // rows > r are still in flight (vmcnt retires in issue order)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int row = min(row0 + r, p.M - 1);
       wv[r] = __builtin_nontemporal_load(
           reinterpret_cast<const u32x4 *>(p.B + (size_t)row * (size_t)row_bytes + (size_t)boff));
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int row = min(row0 + r, p.M - 1);
       const long long b = p.block_base + (((long long)row * p.K + 2 * boff) >> p.bs_log2);
-      if constexpr (DQ) {
+      if constexpr (ABL & 1) {
+        q[r] = (uint32_t)b & 255u;
+        a[r] = 1.0f;
+      } else if constexpr (DQ) {
         q[r] = p.sc.qabsmax[b];
         a[r] = p.sc.absmax2[b >> p.bs2_log2];
       } else {
@@ -243,15 +301,20 @@ template <int MODE, bool DQ, int DT, int R> struct StepLoads {
   }
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4>
-__global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
+__global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p_in) {
+  const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
   constexpr bool kSplit = DT != QZ_DT_F16;
+  constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ float s_part[NW][R];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
 
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  // wave-uniform by construction; readfirstlane makes it provable, so the step
+  // loop compiles to scalar branches instead of exec-masked divergent flow
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int wk = wave % WK;
   const int rg = wave / WK;
   const int row0 = (blockIdx.x * RG + rg) * R;
@@ -265,15 +328,20 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
     offset = *p.sc.offset;
   }
   // 2. this wave's first step of HBM traffic
-  StepLoads<MODE, DQ, DT, R> cur;
+  StepLoads<MODE, DQ, DT, R, XL, ABL> cur;
   int s = wk;
   cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
   const bool have = s < nsteps;
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
     if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
-    __syncthreads();
   }
+  if constexpr (XL) {  // x -> LDS, 16 B per thread per pass
+    const int nchunk = (p.K * XB) >> 4;
+    for (int c = threadIdx.x; c < nchunk; c += NW * 64)
+      reinterpret_cast<u32x4 *>(s_x)[c] = reinterpret_cast<const u32x4 *>(p.x)[c];
+  }
+  if constexpr (DQ || XL) __syncthreads();
 
   uint32_t t[8];
   if (p.lut) {  // runtime codebook -> fp16 byte tables (wave-uniform, once)
@@ -294,29 +362,63 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
 
-  if (have) {
-    for (;; s += WK) {
-      StepLoads<MODE, DQ, DT, R> nxt;
-      const bool more = s + WK < nsteps;
-      if (more) nxt.issue(p, row0, s + WK, lane, row_bytes);
-      uint32_t hi[16], lo[kSplit ? 16 : 1];
-      cur.xs.prepare(hi, lo);
+  // Steady state: the next step's loads are issued UNCONDITIONALLY before the
+  // current step is consumed, and the last step is peeled after the loop.  (A
+  // conditional prefetch makes hipcc's waitcnt pass pick the count valid on
+  // both paths -- vmcnt(0) -- which waits for the prefetch itself and
+  // serialises HBM traffic with the decode.)
+  auto consume = [&](const StepLoads<MODE, DQ, DT, R, XL, ABL> &c) {
+    if constexpr (XL) const_cast<StepLoads<MODE, DQ, DT, R, XL, ABL> &>(c).xs.load_lds(s_x, c.xb);
+    uint32_t hi[16], lo[kSplit ? 16 : 1];
+    c.xs.prepare(hi, lo);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float am;
-        if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cur.q[r]], cur.a[r]), offset);
-        else am = cur.a[r];
-        am = cur.on ? am : 0.0f;
-        acc[r] = fmaf(chunk_dot<MODE, kSplit>(cur.wv[r], hi, lo, t), am, acc[r]);
-      }
-      if (!more) break;
-      cur = nxt;
+    for (int r = 0; r < R; ++r) {
+      float am;
+      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
+      else am = c.a[r];
+      am = c.on ? am : 0.0f;
+      acc[r] = fmaf(chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t), am, acc[r]);
+    }
+  };
+  // Ping-pong over two named load sets (no register copies: copying a
+  // register whose load is in flight forces vmcnt(0)).
+  if (have) {
+    StepLoads<MODE, DQ, DT, R, XL, ABL> other;
+    for (;;) {
+      if (s + WK >= nsteps) { consume(cur); break; }
+      other.issue(p, row0, s + WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the decode
+      consume(cur);
+      s += WK;
+      if (s + WK >= nsteps) { consume(other); break; }
+      cur.issue(p, row0, s + WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(other);
+      s += WK;
     }
   }
 
+  if constexpr ((ABL & 4) != 0) {  // benchmark-only: no reduction, no store
+#pragma unroll
+    for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
+    return;
+  }
+  if constexpr (WK == 1) {  // the wave owns whole rows: no cross-wave pass
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float v = (ABL & 8) ? acc[r] : wave_sum(acc[r]);
+      const int row = row0 + r;
+      if (lane == r && row < p.M) {
+        float o = v * p.out_scale;
+        if (p.bias) o += load_f32<DT>(p.bias, row);
+        store_f32<DT>(p.y, row, o);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float v = wave_sum(acc[r]);
+    const float v = (ABL & 8) ? acc[r] : wave_sum(acc[r]);
     if (lane == 0) s_part[wave][r] = v;
   }
   __syncthreads();
@@ -434,19 +536,27 @@ static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_
 
 using namespace qz;
 
-// Geometry choice shared with the Python side (quantizations_amd/core.py
-// documents it): WK = waves along K (<= steps), R = rows per wave, the largest
-// R that still gives >= 2048 waves (8 per CU) so that every CU keeps >= 32 KiB
-// of weight loads in flight.
-static void choose_geometry(int M, int K, int *R, int *WK) {
+// Geometry (WK = waves along K, R = rows per wave), from the measured sweep in
+// DESIGN.md section 4 (scripts/run_sweep2.sh on MI355X):
+//  * >= 64 Mi weights (8192x8192, 28672x8192, ...): R=4, WK=2 -- fewest
+//    redundant x/scale loads per weight byte, enough waves (>= 8 per CU);
+//  * smaller: R=2; NF4 with WK=1 (no cross-wave reduction), FP4 with WK=2;
+//  * then R halves / WK doubles until the grid has >= 2048 waves, so small-M
+//    slices (TP shards, 1024-row k/v projections) still fill the 256 CUs.
+static void choose_geometry(int M, int K, int mode, int *R, int *WK) {
   const int nsteps = ((K >> 1) + 1023) >> 10;
-  *WK = nsteps >= 4 ? 4 : (nsteps >= 2 ? 2 : 1);
-  *R = 1;
-  for (int r = 4; r >= 2; r >>= 1)
-    if ((long long)((M + r - 1) / r) * (*WK) >= 2048) {
-      *R = r;
-      break;
-    }
+  if ((long long)M * K >= (1LL << 26) && nsteps >= 2) {
+    *R = 4;
+    *WK = 2;
+  } else {
+    *R = 2;
+    *WK = (mode == kModeFP4 && nsteps >= 2) ? 2 : 1;
+  }
+  while ((long long)((M + *R - 1) / *R) * (*WK) < 2048) {
+    if (*R > 1) *R >>= 1;
+    else if (*WK < 4 && *WK * 2 <= nsteps) *WK <<= 1;
+    else break;
+  }
 }
 
 extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
@@ -497,8 +607,8 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   }
 
   int R, WK;
-  choose_geometry(M, K, &R, &WK);
   const int mode = (lut == nullptr && quant_type == QZ_FP4) ? kModeFP4 : kModeLUT16;
+  choose_geometry(M, K, mode, &R, &WK);
   build_tables(mode, quant_type, p.tab, &p.out_scale);
   int rc;
   if (mode == kModeFP4) rc = dq ? dispatch_dt<kModeFP4, true>(p, dtype, R, WK, s) : dispatch_dt<kModeFP4, false>(p, dtype, R, WK, s);

@@ -5,9 +5,85 @@
 // numbers are hipEvent back-to-back averages (kernel + launch gap).
 #include "../../quantizations_amd/csrc/gemv.hip"
 
+namespace qz {
+// Experimental straight-line variant (measured slower than k_gemv_4bit on
+// every decode shape in the round-1 sweep; kept here for reference).  Decode shapes: every wave owns R whole rows
+// (WK = 1) and walks exactly NSW = K / 2048 steps, fully unrolled over two
+// named load sets.  Without runtime control flow hipcc's waitcnt pass sees
+// the exact issue order, so step i+1's HBM loads stay in flight while step i
+// is decoded (the runtime-loop kernel above keeps only ~half a step in
+// flight: its loop-join waits are conservative).
+template <int MODE, bool DQ, int DT, int R, int NSW, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void k_gemv_4bit_sl(GemvParams p_in) {
+  const GemvParams p = load_params(p_in);
+  constexpr bool kSplit = DT != QZ_DT_F16;
+  __shared__ float s_code2[DQ ? 256 : 1];
+
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int row0 = (blockIdx.x * NW + wave) * R;
+  const int row_bytes = p.K >> 1;
+
+  float c2 = 0.0f, offset = 0.0f;
+  if constexpr (DQ) {
+    if (NW * 64 == 256 || threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x & 255];
+    offset = *p.sc.offset;
+  }
+  StepLoads<MODE, DQ, DT, R, false, 0> ld[2];
+  ld[0].issue(p, row0, 0, lane, row_bytes);
+  if constexpr (NSW > 1) ld[1].issue(p, row0, 1, lane, row_bytes);
+  if constexpr (DQ) {
+    if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
+    __syncthreads();
+  }
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
+
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+
+#pragma unroll
+  for (int i = 0; i < NSW; ++i) {
+    StepLoads<MODE, DQ, DT, R, false, 0> &c = ld[i & 1];
+    uint32_t hi[16], lo[kSplit ? 16 : 1];
+    c.xs.prepare(hi, lo);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float am;
+      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
+      else am = c.a[r];
+      am = c.on ? am : 0.0f;
+      acc[r] = fmaf(chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t), am, acc[r]);
+    }
+    if (i + 2 < NSW) {
+      __builtin_amdgcn_sched_barrier(0);
+      c.issue(p, row0, i + 2, lane, row_bytes);  // refill the set just consumed
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float v = wave_sum(acc[r]);
+    const int row = row0 + r;
+    if (lane == r && row < p.M) {
+      float o = v * p.out_scale;
+      if (p.bias) o += load_f32<DT>(p.bias, row);
+      store_f32<DT>(p.y, row, o);
+    }
+  }
+}
+
+}  // namespace qz
+
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <functional>
+#include <string>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
@@ -28,9 +104,24 @@ __global__ __launch_bounds__(T) void k_read_floor(const unsigned char *__restric
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+template <int T, int L>
+__global__ __launch_bounds__(T) void k_read_floor_store(const unsigned char *__restrict__ p, long long bytes, uint32_t *out) {
+  const long long nchunk = bytes / 16;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const long long c = ((long long)blockIdx.x * L + i) * T + threadIdx.x;
+    if (c < nchunk) {
+      v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p) + c);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  if ((threadIdx.x & 63) < 2) out[(blockIdx.x * T + threadIdx.x) / 32] = acc;  // 2 rows' worth per wave
+}
+
 int main(int argc, char **argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, K = argc > 2 ? atoi(argv[2]) : 4096;
-  const int NC = 64, ITERS = 300;
+  const int NC = 64, ITERS = 100;
   const size_t pbytes = (size_t)M * K / 2, nb = (size_t)M * K / 64;
   std::vector<unsigned char *> P(NC), Q(NC);
   std::vector<float *> A2(NC), A(NC);
@@ -45,22 +136,21 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&x, K * 4)); CK(hipMemset(x, 0x3C, K * 4)); CK(hipMalloc(&y, M * 4)); CK(hipMalloc(&sink, 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
 
-  auto timeit = [&](const char *name, auto launch) {
-    for (int i = 0; i < 2 * NC; ++i) launch(i);
-    CK(hipDeviceSynchronize());
-    CK(hipEventRecord(e0));
-    for (int i = 0; i < ITERS; ++i) launch(i);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-    const double us = ms * 1e3 / ITERS;
-    printf("%-44s %8.3f us/launch (b2b)  %7.1f GB/s of %zu B\n", name, us, pbytes / us / 1e3, pbytes);
-  };
-
+  // Variants are registered, then timed in interleaved rounds (rule 24 of the
+  // guide): every round runs each variant for ITERS back-to-back launches;
+  // median and min over rounds are reported.
+  struct Variant { std::string name; std::function<void(int)> launch; std::vector<double> us; };
+  std::vector<Variant> vs;
+  auto timeit = [&](const char *name, auto launch) { vs.push_back({name, launch, {}}); };
 #define FLOOR(T, L) timeit("floor T=" #T " L=" #L, [&](int i) { \
     const long long nchunk = pbytes / 16; const unsigned g = (unsigned)((nchunk + (long long)T * L - 1) / ((long long)T * L)); \
     hipLaunchKernelGGL((k_read_floor<T, L>), dim3(g), dim3(T), 0, 0, P[i % NC], (long long)pbytes, sink); })
-  FLOOR(256, 1); FLOOR(256, 2); FLOOR(256, 4); FLOOR(256, 8); FLOOR(512, 4); FLOOR(1024, 2); FLOOR(1024, 4);
+  const bool sweep = argc > 4 && std::string(argv[4]) == "sweep";
+  FLOOR(256, 1); FLOOR(256, 2);
+  uint32_t *fout; CK(hipMalloc(&fout, 1 << 24));
+  timeit("floor+store T=256 L=2", [&](int i) { const long long nchunk = pbytes / 16;
+    const unsigned g = (unsigned)((nchunk + 511) / 512);
+    hipLaunchKernelGGL((k_read_floor_store<256, 2>), dim3(g), dim3(256), 0, 0, P[i % NC], (long long)pbytes, fout); });
 
   GemvParams p{};
   p.sc = ScaleSrc{nullptr, nullptr, nullptr, code2, off, 256};
@@ -72,12 +162,42 @@ int main(int argc, char **argv) {
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW>), dim3(g), dim3(NW * 64), 0, 0, q); })
 #define GV(MODE, DQ, R, WK) GVN(MODE, DQ, R, WK, 4)
-  GV(1, true, 4, 2); GV(1, true, 2, 2); GV(1, true, 1, 2); GV(1, true, 4, 1); GV(1, true, 2, 1); GV(1, true, 1, 1);
-  GV(1, false, 4, 2); GV(1, false, 2, 2); GV(1, false, 2, 1);
-  GV(2, true, 2, 1); GV(2, false, 2, 1); GV(2, false, 1, 1); GV(2, false, 4, 1); GV(2, false, 2, 2);
-  GVN(2, false, 2, 1, 8); GVN(2, false, 2, 1, 16); GVN(1, true, 2, 1, 8); GVN(1, true, 2, 1, 16); GVN(1, true, 1, 1, 16);
-  GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 16);
+  GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
+  GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
+  GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
+  if (!sweep) { GV(1, false, 2, 2); GV(2, true, 2, 2); }
+#define SL(MODE, R, NSW) timeit("sl mode=" #MODE " R=" #R " NSW=" #NSW, [&](int i) { \
+    GemvParams q = p; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit_sl<MODE, true, QZ_DT_F16, R, NSW>), dim3(g), dim3(256), 0, 0, q); })
+  const int nsw = K / 2048;
+  if (nsw == 2) { SL(1, 1, 2); SL(1, 2, 2); SL(1, 4, 2); }
+  if (nsw == 4) { SL(1, 1, 4); SL(1, 2, 4); SL(1, 4, 4); }
+  if (nsw == 7) { SL(1, 1, 7); SL(1, 2, 7); SL(1, 4, 7); }
+  if (nsw == 14) { SL(1, 1, 14); SL(1, 2, 14); SL(1, 4, 14); }
   build_tables(kModeFP4, QZ_FP4, p.tab, &p.out_scale);
-  GV(0, true, 4, 2); GV(0, true, 2, 2); GV(0, true, 1, 2);
+  GV(0, true, 2, 2); GV(0, true, 4, 2); GV(0, true, 2, 4);
+  if (nsw == 2) { SL(0, 2, 2); SL(0, 4, 2); }
+  if (nsw == 4) { SL(0, 2, 4); SL(0, 4, 4); }
+  if (nsw == 7) { SL(0, 2, 7); SL(0, 4, 7); }
+  if (nsw == 14) { SL(0, 2, 14); SL(0, 4, 14); }
+  const int ROUNDS = argc > 3 ? atoi(argv[3]) : 9;
+  for (auto &v : vs) { for (int i = 0; i < NC; ++i) v.launch(i); }
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < ROUNDS; ++r)
+    for (auto &v : vs) {
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < ITERS; ++i) v.launch(i);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(ms * 1e3 / ITERS);
+    }
+  for (auto &v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    const double med = v.us[v.us.size() / 2], mn = v.us[0];
+    printf("%-48s median %7.3f  min %7.3f us/launch (b2b)  %7.1f GB/s @median\n", v.name.c_str(), med, mn,
+           pbytes / med / 1e3);
+  }
   return 0;
 }

@@ -39,8 +39,12 @@ def main():
     for (name, grid), d in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         e = {"kernel": name[:160], "grid_x": grid, "calls": len(d), "mean_us": round(statistics.mean(d), 3),
              "median_us": round(statistics.median(d), 3), "min_us": round(min(d), 3), "total_us": round(sum(d), 1)}
+        if len(d) >= 10:
+            q = statistics.quantiles(d, n=10)
+            e["p10_us"], e["p90_us"] = round(q[0], 3), round(q[-1], 3)
         out["kernels"].append(e)
-        print(f"{e['calls']:6d} {e['mean_us']:10.3f} {e['median_us']:10.3f} {e['min_us']:9.3f}  grid={grid:>8}  {name[:110]}")
+        print(f"{e['calls']:6d} mean {e['mean_us']:10.3f} med {e['median_us']:10.3f} min {e['min_us']:9.3f} "
+              f"p10 {e.get('p10_us', float('nan')):9.3f} p90 {e.get('p90_us', float('nan')):9.3f}  grid={grid:>8}  {name[:100]}")
     cg = defaultdict(list)
     for r in rows(os.path.join(a.dir, "**", "*counter_collection.csv")):
         name = r.get("Kernel_Name", "")

@@ -251,6 +251,44 @@ def prefill_bench(T: int = 16384, iters: int = 10):
     return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0}
 
 
+@torch.inference_mode()
+def prefill_sweep(Ts=(16, 64, 256, 1024, 2048, 4096, 16384), iters=10):
+    """4096x4096 NF4: fused MFMA GEMM vs dequant + library GEMM over token count T."""
+    from quantizations_amd import _lib
+    from quantizations_amd.core import dequantize_4bit, quantize_4bit
+
+    dev = torch.device("cuda")
+    torch.manual_seed(12)
+    M = K = 4096
+    W = (torch.randn(M, K, device=dev) * 0.02).to(torch.float16)
+    packed, qs = quantize_4bit(W, quant_type="nf4")
+    res = {}
+    for T in Ts:
+        x = torch.randn(T, K, device=dev, dtype=torch.float16)
+        y = torch.empty(T, M, device=dev, dtype=torch.float16)
+
+        def fused():
+            _lib.check(_lib.lib.qz_gemm_4bit(T, M, K, x.data_ptr(), K, _lib.DT_F16, packed.data_ptr(), _lib.NF4, 64,
+                                             *qs.scale_args(), 0, y.data_ptr(), M, _lib.stream_of(x)), "gemm")
+
+        def ref_route():
+            return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
+
+        row = {}
+        for name, fn in (("fused", fused), ("dequant+blas", ref_route)):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            row[name] = round(e0.elapsed_time(e1) / iters * 1e3, 2)
+        res[T] = row
+    return {"shape": "4096x4096 nf4 dq", "us": res}
+
+
 def cpu_baseline(target_s: float = 12.0):
     import numpy as np
 
@@ -293,6 +331,8 @@ def main():
     ap.add_argument("--gemv-only", action="store_true", help="only the 4096x4096 roofline microbench (profiling)")
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--no-prefill", action="store_true")
+    ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
+    ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -313,6 +353,9 @@ def main():
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
         return
+    if args.prefill_sweep:
+        print(json.dumps(prefill_sweep()), flush=True)
+        return
 
     t_build = time.perf_counter()
     model, cfg = build_model(args.layers, seed=0)
@@ -320,6 +363,10 @@ def main():
         from quantizations_amd.parallel import shard_model_linear4bit
         shard_model_linear4bit(model, rank, world)
         torch.cuda.empty_cache()
+    n_groups = 0
+    if not args.no_fuse:
+        from quantizations_amd.integration import fuse_projection_groups
+        n_groups = fuse_projection_groups(model)   # q/k/v and gate/up: one grouped GEMV launch each
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 
@@ -376,7 +423,8 @@ def main():
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
                        "prompt_len": args.prompt, "batch": 1, "decode": mode,
-                       "parallelism": "single" if world == 1 else f"rowsplit-tp{world}-allgather"},
+                       "parallelism": "single" if world == 1 else f"rowsplit-tp{world}-allgather",
+                       "projection_groups": n_groups},
             "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         print(json.dumps(line), flush=True)

@@ -107,6 +107,30 @@ int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B,
                  const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
                  void *y, void *stream);
 
+/* Grouped decode GEMV: several Linear4bit layers that
+ * read the SAME x (q/k/v, or gate/up, of one decoder layer) in ONE launch,
+ * replacing nseg separate modules.py:56-61 calls.  Each segment keeps its own
+ * packed weights, statistics, offset, bias and output y (length M);
+ * K, x, dtype, quant_type, blocksize(2) and lut are shared, and every segment
+ * must use the same scale format (all double-quant or all fp32 absmax).
+ * 1 <= nseg <= QZ_GEMV_MAX_SEGMENTS. */
+#define QZ_GEMV_MAX_SEGMENTS 4
+typedef struct qz_gemv_segment {
+  int M;
+  const unsigned char *B;
+  const float *absmax;          /* fp32 absmax, or NULL with double quant */
+  const unsigned char *qabsmax; /* double quant: u8 codes */
+  const float *absmax2;
+  const float *code2;
+  const float *offset;
+  long long block_base;
+  const void *bias; /* or NULL */
+  void *y;
+} qz_gemv_segment;
+
+int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
+                         int blocksize, int blocksize2, const float *lut, void *stream);
+
 /* Fused 4-bit GEMM (prefill, modules.py:62-64): Y[T,M] = X[T,K] . W[M,K]^T
  * (+ bias) with W dequantised tile-by-tile into LDS and multiplied on MFMA
  * (fp16/bf16 in, fp32 accumulate).  X/Y/bias share `dtype` (F16 or BF16);

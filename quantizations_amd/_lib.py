@@ -30,6 +30,17 @@ _i = ctypes.c_int
 _ll = ctypes.c_longlong
 _f = ctypes.c_float
 
+GEMV_MAX_SEGMENTS = 4  # QZ_GEMV_MAX_SEGMENTS
+
+
+class GemvSegment(ctypes.Structure):
+    """struct qz_gemv_segment (include/quantizations.h)."""
+    _fields_ = [("M", ctypes.c_int), ("B", ctypes.c_void_p), ("absmax", ctypes.c_void_p),
+                ("qabsmax", ctypes.c_void_p), ("absmax2", ctypes.c_void_p), ("code2", ctypes.c_void_p),
+                ("offset", ctypes.c_void_p), ("block_base", ctypes.c_longlong), ("bias", ctypes.c_void_p),
+                ("y", ctypes.c_void_p)]
+
+
 # name -> argtypes (restype int unless noted); mirrors include/quantizations.h
 SIGNATURES = {
     "cgemm_4bit_inference_naive_fp32": [_i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i],
@@ -43,6 +54,7 @@ SIGNATURES = {
     "cquantize_blockwise_fp32_stream": [_p, _p, _p, _p, _i, _i, _p],
     "cdequantize_blockwise_fp32_stream": [_p, _p, _p, _p, _i, _i, _p],
     "qz_gemv_4bit": [_i, _i, _p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _ll, _p, _p, _p, _p],
+    "qz_gemv_4bit_grouped": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p],
     "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p],
     "qz_quantize_4bit": [_p, _i, _ll, _i, _i, _p, _p, _p],
     "qz_absmax_mean_workspace": [_ll],

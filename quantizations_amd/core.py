@@ -21,6 +21,7 @@ What differs, on purpose (DESIGN.md "Host layer"):
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Tuple
 
 import torch
@@ -332,6 +333,50 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
                            state.blocksize, *state.scale_args(), block_base, 0, ptr(bias), ptr(out),
                            _lib.stream_of(A)), "gemv_4bit")
     return out
+
+
+def gemv_4bit_grouped(A: Tensor, items) -> list:
+    """Several batch-1 4-bit GEMVs that share the input vector A, in ONE launch
+    (qz_gemv_4bit_grouped).  items: sequence of
+    (B, state, bias[, block_base[, out]]) with equal K, quant_type, blocksize
+    and scale format; returns [y_i] as gemv_4bit(A, B_i, state=state_i,
+    bias=bias_i, block_base=...) would (`out`, if given, is written in place:
+    a contiguous tensor of M_i elements)."""
+    items = list(items)
+    if not 1 <= len(items) <= _lib.GEMV_MAX_SEGMENTS:
+        raise ValueError(f"gemv_4bit_grouped takes 1..{_lib.GEMV_MAX_SEGMENTS} weights, got {len(items)}")
+    if A.numel() != A.shape[-1]:
+        raise ValueError("gemv_4bit_grouped needs a single input vector")
+    s0 = items[0][1]
+    K = s0.shape[1]
+    if A.shape[-1] != K:
+        raise ValueError(f"A has {A.shape[-1]} features, the 4-bit weights expect {K}")
+    A = A.contiguous()
+    segs = (_lib.GemvSegment * len(items))()
+    outs = []
+    for i, item in enumerate(items):
+        B, st, bias = item[0], item[1], item[2]
+        block_base = int(item[3]) if len(item) > 3 else 0
+        y = item[4] if len(item) > 4 else None
+        if (st.shape[1] != K or st.quant_type != s0.quant_type or st.blocksize != s0.blocksize
+                or st.nested != s0.nested or (st.nested and st.state2.blocksize != s0.state2.blocksize)):
+            raise ValueError("gemv_4bit_grouped: weights must share K, quant_type, blocksize and scale format")
+        M = st.shape[0]
+        if y is None:
+            shape = (A.shape[0], A.shape[1], M) if A.dim() == 3 else (A.shape[0], M) if A.dim() == 2 else (M,)
+            y = torch.empty(shape, dtype=A.dtype, device=A.device)
+        elif y.numel() != M or not y.is_contiguous() or y.dtype != A.dtype:
+            raise ValueError(f"gemv_4bit_grouped: out {i} must be a contiguous {A.dtype} tensor of {M} elements")
+        if bias is not None and bias.dtype != A.dtype:
+            bias = bias.to(A.dtype)
+        am, qam, am2, code2, off, _ = st.scale_args()
+        segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, block_base, ptr(bias), ptr(y))
+        outs.append(y)
+    bs2 = int(s0.state2.blocksize) if s0.nested else 0
+    check(lib.qz_gemv_4bit_grouped(len(items), ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
+                                   _lib.QUANT_TYPES[s0.quant_type], s0.blocksize, bs2, 0, _lib.stream_of(A)),
+          "gemv_4bit_grouped")
+    return outs
 
 
 def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = None) -> Tensor:

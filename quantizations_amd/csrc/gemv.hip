@@ -301,8 +301,10 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoa
   }
 };
 
+// The kernel body, for logical workgroup `block` of one GEMV (a plain launch
+// passes blockIdx.x; a grouped launch passes the block index within its segment).
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
-__global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p_in) {
+__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
   const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
   constexpr bool kSplit = DT != QZ_DT_F16;
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p_in) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int wk = wave % WK;
   const int rg = wave / WK;
-  const int row0 = (blockIdx.x * RG + rg) * R;
+  const int row0 = (block * RG + rg) * R;
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
 
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p_in) {
   __syncthreads();
   if ((int)threadIdx.x < RG * R) {
     const int g = threadIdx.x / R, r = threadIdx.x % R;
-    const int row = (blockIdx.x * RG + g) * R + r;
+    const int row = (block * RG + g) * R + r;
     if (row < p.M) {
       float v = 0.0f;
 #pragma unroll
@@ -434,6 +436,39 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p_in) {
       store_f32<DT>(p.y, row, v);
     }
   }
+}
+
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
+__global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL>(p, blockIdx.x);
+}
+
+// Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
+// one decoder layer) in ONE grid.  Segment i owns workgroups
+// [start[i], start[i+1]); each segment keeps its own weights, statistics,
+// offset, bias and output, so every output is bit-identical to its own
+// qz_gemv_4bit launch with the same geometry.
+constexpr int kMaxSeg = 4;
+struct GemvGroup {
+  GemvParams seg[kMaxSeg];
+  int start[kMaxSeg];
+  int nseg;
+};
+
+template <int MODE, bool DQ, int DT, int R, int WK>
+__global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
+  const int b = blockIdx.x;
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxSeg; ++i)
+    if (i < g.nseg && b >= g.start[i]) s = i;
+  s = __builtin_amdgcn_readfirstlane(s);
+  // copy the segment out before load_params launders it: loads through a
+  // computed kernarg address are not invariant, so interleaving them with the
+  // laundering asm would serialise them (one s_waitcnt per field)
+  const GemvParams seg = g.seg[s];
+  const int start = g.start[s];
+  gemv_body<MODE, DQ, DT, R, WK>(seg, b - start);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -559,10 +594,12 @@ static void choose_geometry(int M, int K, int mode, int *R, int *WK) {
   }
 }
 
-extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
-                            int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
-                            const float *code2, const float *offset, int blocksize2, long long block_base,
-                            const float *lut, const void *bias, void *y, void *stream) {
+// Validates one GEMV's arguments and fills its kernel parameters (everything
+// except the decode tables).  Returns QZ_OK or a negative status.
+static int make_params(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type, int blocksize,
+                       const float *absmax, const unsigned char *qabsmax, const float *absmax2, const float *code2,
+                       const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
+                       void *y, GemvParams *p, bool *vec_ok) {
   if (!x || !B || !y || M < 0 || K < 0) return QZ_ERR_ARG;
   if ((absmax == nullptr) == (qabsmax == nullptr)) return QZ_ERR_ARG;
   const bool dq = qabsmax != nullptr;
@@ -572,25 +609,35 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   const int bsl = ilog2(blocksize);
   const int bs2l = dq ? ilog2(blocksize2) : 0;
   if (bsl < 1 || bs2l < 0) return QZ_ERR_BLOCKSIZE;
+  p->B = B;
+  p->x = x;
+  p->sc = ScaleSrc{absmax, qabsmax, absmax2, code2, offset, blocksize2};
+  p->bias = bias;
+  p->y = y;
+  p->lut = lut;
+  p->block_base = block_base;
+  p->M = M;
+  p->K = K;
+  p->bs_log2 = bsl;
+  p->bs2_log2 = bs2l;
+  *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
+            (reinterpret_cast<uintptr_t>(x) % 16) == 0;
+  return QZ_OK;
+}
+
+extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
+                            int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
+                            const float *code2, const float *offset, int blocksize2, long long block_base,
+                            const float *lut, const void *bias, void *y, void *stream) {
+  GemvParams p;
+  bool vec_ok;
+  const int st = make_params(M, K, x, dtype, B, quant_type, blocksize, absmax, qabsmax, absmax2, code2, offset,
+                             blocksize2, block_base, lut, bias, y, &p, &vec_ok);
+  if (st != QZ_OK) return st;
   if (M == 0) return QZ_OK;
+  const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
 
-  GemvParams p;
-  p.B = B;
-  p.x = x;
-  p.sc = ScaleSrc{absmax, qabsmax, absmax2, code2, offset, blocksize2};
-  p.bias = bias;
-  p.y = y;
-  p.lut = lut;
-  p.block_base = block_base;
-  p.M = M;
-  p.K = K;
-  p.bs_log2 = bsl;
-  p.bs2_log2 = bs2l;
-
-  const bool vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 &&
-                      (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
-                      (reinterpret_cast<uintptr_t>(x) % 16) == 0;
   if (!vec_ok) {
     const unsigned grid = (unsigned)((M + 3) / 4);
     if (K == 0) return QZ_ERR_SHAPE;
@@ -614,6 +661,69 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   if (mode == kModeFP4) rc = dq ? dispatch_dt<kModeFP4, true>(p, dtype, R, WK, s) : dispatch_dt<kModeFP4, false>(p, dtype, R, WK, s);
   else rc = dq ? dispatch_dt<kModeLUT16, true>(p, dtype, R, WK, s) : dispatch_dt<kModeLUT16, false>(p, dtype, R, WK, s);
   if (rc != QZ_OK) return rc;
+  QZ_LAUNCH_CHECK();
+  return QZ_OK;
+}
+
+extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
+                                    int quant_type, int blocksize, int blocksize2, const float *lut, void *stream) {
+  if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
+  GemvGroup g;
+  g.nseg = nseg;
+  bool all_vec = true;
+  long long total_m = 0;
+  const bool dq = segs[0].qabsmax != nullptr;
+  for (int i = 0; i < nseg; ++i) {
+    const qz_gemv_segment &q = segs[i];
+    bool v;
+    const int st = make_params(q.M, K, x, dtype, q.B, quant_type, blocksize, q.absmax, q.qabsmax, q.absmax2, q.code2,
+                               q.offset, blocksize2, q.block_base, lut, q.bias, q.y, &g.seg[i], &v);
+    if (st != QZ_OK) return st;
+    if ((q.qabsmax != nullptr) != dq) return QZ_ERR_ARG;  // one launch = one scale format
+    all_vec = all_vec && v;
+    total_m += q.M;
+  }
+  if (total_m == 0) return QZ_OK;
+  if (!all_vec || total_m > INT32_MAX) {  // odd shapes: one launch per segment (same results)
+    for (int i = 0; i < nseg; ++i) {
+      const qz_gemv_segment &q = segs[i];
+      const int rc = qz_gemv_4bit(q.M, K, x, dtype, q.B, quant_type, blocksize, q.absmax, q.qabsmax, q.absmax2,
+                                  q.code2, q.offset, blocksize2, q.block_base, lut, q.bias, q.y, stream);
+      if (rc != QZ_OK) return rc;
+    }
+    return QZ_OK;
+  }
+  int R, WK;
+  const int mode = (lut == nullptr && quant_type == QZ_FP4) ? kModeFP4 : kModeLUT16;
+  choose_geometry((int)total_m, K, mode, &R, &WK);
+  const int rows_per_block = R * (4 / WK);
+  int blocks = 0;
+  for (int i = 0; i < nseg; ++i) {
+    build_tables(mode, quant_type, g.seg[i].tab, &g.seg[i].out_scale);
+    g.start[i] = blocks;
+    blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
+  }
+  for (int i = nseg; i < kMaxSeg; ++i) g.start[i] = blocks;
+  hipStream_t s = (hipStream_t)stream;
+#define QZ_GR(MODE_, DQ_, DT_, RR, WW) \
+  hipLaunchKernelGGL((k_gemv_4bit_grouped<MODE_, DQ_, DT_, RR, WW>), dim3(blocks), dim3(256), 0, s, g)
+#define QZ_GR_RW(MODE_, DQ_, DT_)                                                                   \
+  do {                                                                                            \
+    if (WK == 4) { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 4); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 4); else QZ_GR(MODE_, DQ_, DT_, 1, 4); } \
+    else if (WK == 2) { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 2); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 2); else QZ_GR(MODE_, DQ_, DT_, 1, 2); } \
+    else { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 1); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 1); else QZ_GR(MODE_, DQ_, DT_, 1, 1); } \
+  } while (0)
+#define QZ_GR_DT(MODE_, DQ_)                                  \
+  do {                                                      \
+    if (dtype == QZ_DT_F16) QZ_GR_RW(MODE_, DQ_, QZ_DT_F16);  \
+    else if (dtype == QZ_DT_BF16) QZ_GR_RW(MODE_, DQ_, QZ_DT_BF16); \
+    else QZ_GR_RW(MODE_, DQ_, QZ_DT_F32);                     \
+  } while (0)
+  if (mode == kModeFP4) { if (dq) QZ_GR_DT(kModeFP4, true); else QZ_GR_DT(kModeFP4, false); }
+  else { if (dq) QZ_GR_DT(kModeLUT16, true); else QZ_GR_DT(kModeLUT16, false); }
+#undef QZ_GR_DT
+#undef QZ_GR_RW
+#undef QZ_GR
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

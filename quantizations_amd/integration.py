@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .core import Params4bit
-from .modules import Linear4bit
+from .modules import DecodeGroup, Linear4bit, _linear4bit_group_compute
 
 
 def _cfg(quantization_config, name, default):
@@ -61,3 +61,63 @@ def replace_with_bnb_linear(model: nn.Module, modules_to_not_convert: Optional[I
 
 # the name used by transformers (README.md:67)
 _replace_with_bnb_linear = replace_with_bnb_linear
+
+
+# projections of one block that read the same input (Llama/Mistral/Qwen naming,
+# plus the Mixtral-style w1/w3 expert pair)
+DEFAULT_PROJECTION_GROUPS = (("q_proj", "k_proj", "v_proj"), ("gate_proj", "up_proj"), ("w1", "w3"))
+
+
+def _group_compatible(members) -> bool:
+    from .parallel import RowShardedLinear4bit
+
+    cls = type(members[0])
+    if any(type(m) is not cls for m in members):
+        return False
+    if cls is Linear4bit:
+        states = [m.weight.quant_state for m in members]
+        if any(s is None for s in states):
+            return False
+        if len({m.compute_dtype for m in members}) != 1:
+            return False
+    elif cls is RowShardedLinear4bit:
+        states = [m.state for m in members]
+        if len({(m.world_size, id(m.group)) for m in members}) != 1 or \
+                any(m._local_matmul is not members[0]._local_matmul for m in members):
+            return False
+    else:
+        return False
+    s0 = states[0]
+    return all(s.shape[1] == s0.shape[1] and s.quant_type == s0.quant_type and s.blocksize == s0.blocksize
+               and s.nested == s0.nested and (not s.nested or s.state2.blocksize == s0.state2.blocksize)
+               for s in states)
+
+
+def fuse_projection_groups(model: nn.Module, groups=DEFAULT_PROJECTION_GROUPS) -> int:
+    """Attach a DecodeGroup to every set of sibling 4-bit projections named in
+    `groups` (e.g. q/k/v and gate/up of each decoder layer) so that batch-1
+    decode issues ONE grouped GEMV per set (and, for row-sharded layers, one
+    all-gather per set).  Works on Linear4bit and on RowShardedLinear4bit (call
+    it after ``parallel.shard_model_linear4bit``).  Prefill is unchanged.
+    Returns the number of groups formed."""
+    from .parallel import RowShardedLinear4bit, sharded_group_compute
+
+    n = 0
+    for parent in model.modules():
+        for names in groups:
+            members = [parent._modules.get(nm) for nm in names]
+            if any(m is None for m in members) or not _group_compatible(members):
+                continue
+            compute = _linear4bit_group_compute if isinstance(members[0], Linear4bit) else sharded_group_compute
+            assert isinstance(members[0], (Linear4bit, RowShardedLinear4bit))
+            g = DecodeGroup(members, compute)
+            for m in members:
+                m.__dict__["_qz_group"] = g
+            n += 1
+    return n
+
+
+def unfuse_projection_groups(model: nn.Module) -> None:
+    """Remove every DecodeGroup attached by fuse_projection_groups."""
+    for m in model.modules():
+        m.__dict__.pop("_qz_group", None)

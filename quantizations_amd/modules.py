@@ -8,11 +8,13 @@ dequantised copy of W is ever materialised in HBM on the supported shapes.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn as nn
 
 from . import _lib
-from .core import Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemv_4bit
+from .core import Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemv_4bit, gemv_4bit_grouped
 
 
 def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None):
@@ -22,6 +24,53 @@ def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: 
     if A.numel() == A.shape[-1]:
         return gemv_4bit(A, B, out, state=quant_state, bias=bias)
     return gemm_4bit(A, B, quant_state, bias=bias)
+
+
+class DecodeGroup:
+    """Linear4bit layers that read the same input (q/k/v or gate/up of one
+    decoder layer), fused for batch-1 decode into one grouped GEMV launch
+    (SURVEY.md 8f row 2).  The first member called with a decode-shaped x
+    computes every member's output; the others pick theirs up if they are
+    called with the SAME tensor object (identity + version check, so a new or
+    modified input always recomputes).  Prefill inputs bypass the group.
+    Built by ``integration.fuse_projection_groups``."""
+
+    def __init__(self, members, compute):
+        self.members = list(members)
+        self._compute = compute          # (group, x) -> list of outputs, one per member
+        self._x = None                   # weakref to the input the cached outputs belong to
+        self._ver = -1
+        self._outs = {}
+
+    @staticmethod
+    def _version(x: torch.Tensor) -> int:
+        # inference-mode tensors carry no version counter: identity alone keys them
+        return -2 if x.is_inference() else x._version
+
+    def take(self, member, x: torch.Tensor) -> torch.Tensor:
+        key = id(member)
+        ver = self._version(x)
+        if self._x is None or self._x() is not x or self._ver != ver or key not in self._outs:
+            outs = self._compute(self, x)
+            self._outs = {id(m): o for m, o in zip(self.members, outs)}
+            self._x = weakref.ref(x)
+            self._ver = ver
+        out = self._outs.pop(key)
+        if not self._outs:
+            self._x = None
+        return out
+
+
+def _linear4bit_group_compute(group: DecodeGroup, x: torch.Tensor):
+    m0 = group.members[0]
+    inp_dtype = x.dtype
+    xin = m0._input(x)
+    items = []
+    for m in group.members:
+        bias = None if m.bias is None else m.bias.to(xin.dtype)
+        items.append((m.weight, m.weight.quant_state, bias))
+    outs = gemv_4bit_grouped(xin, items)
+    return [o if o.dtype == inp_dtype else o.to(inp_dtype) for o in outs]
 
 
 class Linear4bit(nn.Linear):
@@ -61,6 +110,9 @@ class Linear4bit(nn.Linear):
         qs = self.weight.quant_state
         if qs is None:
             raise RuntimeError("Linear4bit weight is not quantised yet: move the module to a GPU first")
+        group = self.__dict__.get("_qz_group")
+        if group is not None and x.numel() == x.shape[-1]:
+            return group.take(self, x)
         inp_dtype = x.dtype
         xin = self._input(x)
         bias = None if self.bias is None else self.bias.to(xin.dtype)

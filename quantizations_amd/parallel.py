@@ -104,6 +104,9 @@ class RowShardedLinear4bit(nn.Module):
         return gemm_4bit(x, self.packed, self.state, bias=self.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        group = self.__dict__.get("_qz_group")
+        if group is not None and x.numel() == x.shape[-1]:
+            return group.take(self, x)
         y = self.local_forward(x)                       # [..., M/P]
         lead = y.shape[:-1]
         rows = y.shape[-1]
@@ -115,6 +118,39 @@ class RowShardedLinear4bit(nn.Module):
             return gathered.reshape(*lead, self.world_size * rows)
         full = gathered.view(self.world_size, T, rows).permute(1, 0, 2).reshape(T, self.world_size * rows)
         return full.reshape(*lead, self.world_size * rows)
+
+
+def sharded_group_compute(group, x: torch.Tensor):
+    """Decode step of a DecodeGroup of RowShardedLinear4bit layers: ONE grouped
+    local GEMV writes every member's row shard into one buffer, ONE all-gather
+    exchanges it (instead of one all-gather per layer: bs=1 decode collectives
+    are latency-bound), then each member's full output is cut out of the
+    [world, sum(rows)] result."""
+    from .core import gemv_4bit_grouped
+
+    ms = group.members
+    rows = [m.r1 - m.r0 for m in ms]
+    S = sum(rows)
+    buf = torch.empty(S, dtype=x.dtype, device=x.device)
+    views, o = [], 0
+    for r in rows:
+        views.append(buf[o:o + r])
+        o += r
+    if ms[0]._local_matmul is not None:  # test hook (CPU): per-member local matmul
+        for m, v in zip(ms, views):
+            v.copy_(m._local_matmul(x, m).reshape(-1))
+    else:
+        gemv_4bit_grouped(x, [(m.packed, m.state, m.bias, m.block_base, v) for m, v in zip(ms, views)])
+    P = ms[0].world_size
+    gathered = torch.empty(P * S, dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(gathered, buf, group=ms[0].group)
+    g2 = gathered.view(P, S)
+    lead = x.shape[:-1]
+    outs, o = [], 0
+    for r in rows:
+        outs.append(g2[:, o:o + r].reshape(*lead, P * r))
+        o += r
+    return outs
 
 
 def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,

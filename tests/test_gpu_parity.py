@@ -34,13 +34,19 @@ def _ulp(dtype):
 
 def assert_close(y, yref, dtype, what=""):
     """1e-3 relative (north_star) on the fp32-accumulated result.  A bf16 output
-    cannot carry 1e-3 (its own rounding is up to 2^-9), so for bf16 the
-    reference is rounded to bf16 first and the bar applies to the difference."""
+    cannot carry 1e-3 (its own rounding is up to 2^-9, and an fp32 result a
+    hair away from the reference's may round to the other bf16 neighbour), so
+    for bf16 the norm bar applies after removing the output format's own
+    1-ulp rounding from each element."""
     y = np.asarray(y, np.float64).ravel()
     yref = np.asarray(yref, np.float64).ravel()
     if dtype == torch.bfloat16:
+        d = y - yref
+        ulp = np.exp2(np.floor(np.log2(np.maximum(np.abs(yref), 1e-30))) - 7)
+        rel = np.linalg.norm(np.sign(d) * np.maximum(np.abs(d) - ulp, 0)) / max(np.linalg.norm(yref), 1e-30)
         yref = torch.from_numpy(yref).to(torch.bfloat16).double().numpy()
-    rel = np.linalg.norm(y - yref) / max(np.linalg.norm(yref), 1e-30)
+    else:
+        rel = np.linalg.norm(y - yref) / max(np.linalg.norm(yref), 1e-30)
     assert rel <= REL_TOL, f"{what}: rel err {rel:.3e}"
     bound = 1e-3 * np.max(np.abs(yref)) + _ulp(dtype) * np.abs(yref) + 1e-30
     worst = np.max(np.abs(y - yref) - bound)
@@ -293,6 +299,89 @@ def test_gemv_row_shard_block_base(orc):
             assert torch.equal(y, full[:, sh.r0:sh.r1]), (world, r)
 
 
+GROUPED_SETS = [  # (segment rows, K): Llama-3-8B q/k/v and gate/up, plus odd and tiny cases
+    ((4096, 1024, 1024), 4096), ((14336, 14336), 4096), ((512, 128, 128), 1024), ((37, 5, 64, 3), 2112),
+    ((7, 9), 96), ((3, 4), 62)]
+
+
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("dq", [True, False])
+@pytest.mark.parametrize("rows,K", GROUPED_SETS)
+def test_gemv_grouped_matches_oracle(orc, qt, dq, rows, K):
+    """One grouped launch (q/k/v-style segments sharing x) == each layer's oracle GEMV."""
+    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, quantize_4bit
+
+    x = _x(K, seed=K + 5).to(DEV).reshape(1, 1, K)
+    items, refs = [], []
+    for i, M in enumerate(rows):
+        W = _w(M, K, seed=100 + 7 * i + M)
+        packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+        bias = torch.randn(M, generator=torch.Generator().manual_seed(i)).half().to(DEV) if i == 1 else None
+        items.append((packed, st, bias))
+        o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=dq)
+        r = orc.gemv(x.float().cpu().numpy().ravel(), o).astype(np.float32)
+        refs.append(r + (bias.float().cpu().numpy() if bias is not None else 0))
+    ys = gemv_4bit_grouped(x, items)
+    for i, (y, r) in enumerate(zip(ys, refs)):
+        assert y.shape == (1, 1, rows[i]) and y.dtype == torch.float16
+        assert_close(y.float().cpu(), r, torch.float16, f"segment {i} {qt} dq={dq} rows={rows} K={K}")
+        single = gemv_4bit(x, items[i][0], state=items[i][1], bias=items[i][2])
+        assert_close(y.float().cpu(), single.float().cpu().numpy(), torch.float16, f"vs single {i}")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemv_grouped_activation_dtypes_and_out(orc, dtype):
+    from quantizations_amd.core import gemv_4bit_grouped, quantize_4bit
+
+    K = 2048
+    x = _x(K, seed=3, dtype=dtype).to(DEV).reshape(1, K)
+    rows = (1000, 24)
+    buf = torch.full((sum(rows),), float("nan"), dtype=dtype, device=DEV)
+    items, refs, o0 = [], [], 0
+    for i, M in enumerate(rows):
+        W = _w(M, K, seed=50 + i)
+        packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+        items.append((packed, st, None, 0, buf[o0:o0 + M]))
+        o0 += M
+        refs.append(orc.gemv(x.float().cpu().numpy().ravel(), orc.quantize_4bit(W.float().numpy(), 64, "nf4")))
+    ys = gemv_4bit_grouped(x, items)
+    assert ys[0].data_ptr() == buf.data_ptr()  # written in place
+    for y, r in zip(ys, refs):
+        assert_close(y.float().cpu(), r, dtype, f"grouped {dtype}")
+
+
+def test_gemv_grouped_rejects_mismatched_weights():
+    from quantizations_amd.core import gemv_4bit_grouped, quantize_4bit
+
+    x = torch.randn(1, 256, device=DEV, dtype=torch.float16)
+    a = quantize_4bit(_w(64, 256).to(DEV), quant_type="nf4")
+    b = quantize_4bit(_w(64, 512).to(DEV), quant_type="nf4")
+    c = quantize_4bit(_w(64, 256).to(DEV), quant_type="nf4", compress_statistics=False)
+    with pytest.raises(ValueError):
+        gemv_4bit_grouped(x, [(a[0], a[1], None), (b[0], b[1], None)])       # different K
+    with pytest.raises(ValueError):
+        gemv_4bit_grouped(x, [(a[0], a[1], None), (c[0], c[1], None)])       # DQ vs fp32 absmax
+    with pytest.raises(ValueError):
+        gemv_4bit_grouped(x, [(a[0], a[1], None)] * 5)                       # > QZ_GEMV_MAX_SEGMENTS
+
+
+def test_gemv_grouped_row_shards(orc):
+    """Row shards (block_base != 0) of three layers in one grouped launch."""
+    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, quantize_4bit
+    from quantizations_amd.parallel import shard_rows
+
+    K = 640
+    x = _x(K, seed=61).to(DEV).reshape(1, K)
+    fulls, shards = [], []
+    for i, M in enumerate((96, 32, 64)):
+        packed, st = quantize_4bit(_w(M, K, seed=70 + i).to(DEV), quant_type="nf4")
+        fulls.append(gemv_4bit(x, packed, state=st))
+        shards.append(shard_rows(packed, st, 1, 2))
+    ys = gemv_4bit_grouped(x, [(sh.packed, sh.state, None, sh.block_base) for sh in shards])
+    for y, f, sh in zip(ys, fulls, shards):
+        assert_close(y.float().cpu(), f[:, sh.r0:sh.r1].float().cpu().numpy(), torch.float16, "grouped shard")
+
+
 # ---------------------------------------------------------------------------
 # fused prefill GEMM (MFMA)
 # ---------------------------------------------------------------------------
@@ -412,3 +501,69 @@ def test_tiny_llama_with_linear4bit(orc):
         out_ref = ref(input_ids=ids).logits.float()
     rel = (out - out_ref).norm() / out_ref.norm()
     assert rel < 5e-3, rel
+
+
+def test_tiny_llama_fused_projection_groups(orc):
+    """fuse_projection_groups (q/k/v and gate/up in one launch each): greedy
+    decode tokens and logits match the unfused model; also under HIP-graph
+    capture of the decode step."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import (fuse_projection_groups, replace_with_bnb_linear,
+                                               unfuse_projection_groups)
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=512)
+    torch.manual_seed(1)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, quant_type="nf4", compute_dtype=torch.float32)
+    ids = torch.randint(0, 512, (1, 8), device=DEV)
+    with torch.no_grad():
+        ref = model(input_ids=ids, use_cache=True)
+        tok = ref.logits[:, -1:].argmax(-1)
+        ref_step = model(input_ids=tok, past_key_values=ref.past_key_values, use_cache=True).logits.float()
+        tok2 = ref_step[:, -1:].argmax(-1)
+        ref_step2 = model(input_ids=tok2, past_key_values=ref.past_key_values, use_cache=True).logits.float()
+        assert fuse_projection_groups(model) == 2 * cfg.num_hidden_layers
+        out = model(input_ids=ids, use_cache=True)     # prefill bypasses the groups
+        assert torch.equal(out.logits, ref.logits)
+        # two decode steps: each step's new input must recompute the groups
+        for t, r in ((tok, ref_step), (tok2, ref_step2)):
+            step = model(input_ids=t, past_key_values=out.past_key_values, use_cache=True).logits.float()
+            rel = (step - r).norm() / r.norm()
+            assert rel < 2e-3, rel
+        unfuse_projection_groups(model)
+        assert all("_qz_group" not in m.__dict__ for m in model.modules())
+
+
+def test_fused_groups_hip_graph_capture():
+    """Grouped q/k/v inside a captured graph: replays follow new inputs."""
+    import quantizations_amd as qa
+    from quantizations_amd.integration import fuse_projection_groups
+
+    parent = torch.nn.Module()
+    for name, M in (("q_proj", 2048), ("k_proj", 512), ("v_proj", 512)):
+        parent.add_module(name, qa.Linear4bit(2048, M, quant_type="nf4").half().to(DEV))
+    assert fuse_projection_groups(parent) == 1
+    x = torch.randn(1, 1, 2048, device=DEV, dtype=torch.float16)
+
+    def run():
+        return parent.q_proj(x), parent.k_proj(x), parent.v_proj(x)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            run()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        outs = run()
+    x.copy_(torch.randn_like(x))
+    g.replay()
+    torch.cuda.synchronize()
+    for o, name in zip(outs, ("q_proj", "k_proj", "v_proj")):
+        m = getattr(parent, name)
+        ref = torch.nn.functional.linear(x.float(), m.dequantize().float())
+        rel = (o.float() - ref).norm() / ref.norm()
+        assert rel < 2e-3, (name, rel)

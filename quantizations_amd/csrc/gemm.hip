@@ -31,7 +31,6 @@ constexpr int kBT = 128, kBM = 128, kBK = 64;
 __device__ __forceinline__ uint32_t gperm(uint32_t s0, uint32_t s1, uint32_t sel) {
   return __builtin_amdgcn_perm(s0, s1, sel);
 }
-__device__ __forceinline__ uint32_t gbfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
 // 8 nibbles -> 4 natural-order half2 (e_2j, e_2j+1) of the unscaled codebook
 // (FP4: values x12, exact; 16-entry: fp16 of the codebook).
@@ -45,15 +44,17 @@ __device__ __forceinline__ void decode_nat(uint32_t w, const uint32_t (&t)[8], u
     P[2] = gperm(hh, hl, 0x020C060Cu);
     P[3] = gperm(hh, hl, 0x030C070Cu);
   } else {
-    const uint32_t sh = (w >> 4) & 0x07070707u;
-    const uint32_t mh = gperm(w << 8, w, 0x090B080Au);
-    const uint32_t lh = gbfi(mh, gperm(t[3], t[2], sh), gperm(t[1], t[0], sh));
-    const uint32_t hh = gbfi(mh, gperm(t[7], t[6], sh), gperm(t[5], t[4], sh));
-    const uint32_t w4 = w << 4;
-    const uint32_t sl = w & 0x07070707u;
-    const uint32_t ml = gperm(w4 << 8, w4, 0x090B080Au);
-    const uint32_t ll = gbfi(ml, gperm(t[3], t[2], sl), gperm(t[1], t[0], sl));
-    const uint32_t hl = gbfi(ml, gperm(t[7], t[6], sl), gperm(t[5], t[4], sl));
+    // AND-combined 8-entry lookups (see decode_lut16 in gemv.hip)
+    uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);
+    asm("" : "+v"(ah));
+    const uint32_t bh = ah ^ 0x88888888u;
+    const uint32_t lh = gperm(t[1], t[0], ah) & gperm(t[3], t[2], bh);
+    const uint32_t hh = gperm(t[5], t[4], ah) & gperm(t[7], t[6], bh);
+    uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);
+    asm("" : "+v"(al));
+    const uint32_t bl = al ^ 0x88888888u;
+    const uint32_t ll = gperm(t[1], t[0], al) & gperm(t[3], t[2], bl);
+    const uint32_t hl = gperm(t[5], t[4], al) & gperm(t[7], t[6], bl);
     const uint32_t q0 = gperm(hh, lh, 0x05010400u);  // (e0, e2)
     const uint32_t q1 = gperm(hh, lh, 0x07030602u);  // (e4, e6)
     const uint32_t q2 = gperm(hl, ll, 0x05010400u);  // (e1, e3)

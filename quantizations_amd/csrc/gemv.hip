@@ -38,7 +38,11 @@
 
 namespace qz {
 
-enum { kModeFP4 = 0, kModeLUT16 = 1, kModeRaw = 2 /* benchmark-only: no decode */ };
+enum {
+  kModeFP4 = 0,    // sign/magnitude FP4: 8-entry x12 table in VALU
+  kModeLUT16 = 1,  // any 16-entry codebook (NF4): AND-combined v_perm lookups in VALU
+  kModeRaw = 2     // benchmark-only: no decode
+};
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -118,16 +122,23 @@ __device__ __forceinline__ void decode_fp4(uint32_t w, uint32_t t0, uint32_t t1,
 }
 
 // 16-entry codebook: 8 nibbles -> (e0,e2),(e4,e6),(e1,e3),(e5,e7).
+// Each fp16 byte plane is a 16-entry lookup done as two 8-entry v_perm
+// lookups AND-ed together: the selector byte is the nibble with its bit 3
+// copied to bit 7, so entries 0-7 index the first table directly and
+// entries 8-15 give a selector >= 0x88, which v_perm maps to 0xFF; XOR 0x88
+// swaps the roles for the second table.  (v_perm, v_bfi and v_dot2c issue at
+// half rate on gfx950; this form needs no mask perm and no v_bfi.)
 __device__ __forceinline__ void decode_lut16(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
-  const uint32_t sh = (w >> 4) & 0x07070707u;
-  const uint32_t mh = perm(w << 8, w, 0x090B080Au);  // 0xFF per byte where the high nibble has bit 3
-  const uint32_t lh = bfi(mh, perm(t[3], t[2], sh), perm(t[1], t[0], sh));
-  const uint32_t hh = bfi(mh, perm(t[7], t[6], sh), perm(t[5], t[4], sh));
-  const uint32_t w4 = w << 4;
-  const uint32_t sl = w & 0x07070707u;
-  const uint32_t ml = perm(w4 << 8, w4, 0x090B080Au);
-  const uint32_t ll = bfi(ml, perm(t[3], t[2], sl), perm(t[1], t[0], sl));
-  const uint32_t hl = bfi(ml, perm(t[7], t[6], sl), perm(t[5], t[4], sl));
+  uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);   // high nibbles (even elements)
+  asm("" : "+v"(ah));  // keep the XOR below a full-rate v_xor (not a re-associated v_bitop3)
+  const uint32_t bh = ah ^ 0x88888888u;
+  const uint32_t lh = perm(t[1], t[0], ah) & perm(t[3], t[2], bh);
+  const uint32_t hh = perm(t[5], t[4], ah) & perm(t[7], t[6], bh);
+  uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);   // low nibbles (odd elements)
+  asm("" : "+v"(al));
+  const uint32_t bl = al ^ 0x88888888u;
+  const uint32_t ll = perm(t[1], t[0], al) & perm(t[3], t[2], bl);
+  const uint32_t hl = perm(t[5], t[4], al) & perm(t[7], t[6], bl);
   P[0] = perm(hh, lh, 0x05010400u);
   P[1] = perm(hh, lh, 0x07030602u);
   P[2] = perm(hl, ll, 0x05010400u);
@@ -143,9 +154,9 @@ template <int MODE, int DT> struct XSlice {
   static constexpr int kWords = DT == QZ_DT_F32 ? 32 : 16;  // raw dwords per lane
   uint32_t raw[kWords];
 
-  __device__ __forceinline__ void load(const void *x, long long e0) {
+  __device__ __forceinline__ void load(const void *x, uint32_t e0) {
     const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(x) +
-                                                     e0 * (DT == QZ_DT_F32 ? 4 : 2));
+                                                     e0 * (DT == QZ_DT_F32 ? 4u : 2u));
 #pragma unroll
     for (int i = 0; i < kWords / 4; ++i) {
       const u32x4 v = p[i];
@@ -270,26 +281,29 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoa
   int xb;  // first activation index of this lane's chunk
   bool on;
 
+  // All offsets are 32-bit unsigned (the launcher guarantees M*K < 2^32): the
+  // loads then use the SGPR-base + 32-bit VGPR offset form, with no 64-bit
+  // VALU address arithmetic per load.
   __device__ __forceinline__ void issue(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
-    const int boff_raw = (s << 10) + (lane << 4);
-    on = boff_raw < row_bytes;
-    const int boff = on ? boff_raw : 0;
-    xb = 2 * boff;
-    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2LL * boff);
+    const uint32_t boff_raw = ((uint32_t)s << 10) + ((uint32_t)lane << 4);
+    on = boff_raw < (uint32_t)row_bytes;
+    const uint32_t boff = on ? boff_raw : 0u;
+    xb = 2 * (int)boff;
+    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2u * boff);
     if constexpr (ABL & 2) {
 #pragma unroll
-      for (int i = 0; i < XSlice<MODE, DT>::kWords; ++i) xs.raw[i] = 0x3C003C00u ^ (uint32_t)boff;
+      for (int i = 0; i < XSlice<MODE, DT>::kWords; ++i) xs.raw[i] = 0x3C003C00u ^ boff;
     }
     // per row: weights then that row's scale, so row r can be consumed while
     // rows > r are still in flight (vmcnt retires in issue order)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int row = min(row0 + r, p.M - 1);
-      wv[r] = __builtin_nontemporal_load(
-          reinterpret_cast<const u32x4 *>(p.B + (size_t)row * (size_t)row_bytes + (size_t)boff));
-      const long long b = p.block_base + (((long long)row * p.K + 2 * boff) >> p.bs_log2);
+      const uint32_t row = (uint32_t)min(row0 + r, p.M - 1);  // wave-uniform
+      const unsigned char *rowp = p.B + (size_t)row * (uint32_t)row_bytes;
+      wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + boff));
+      const uint32_t b = (uint32_t)p.block_base + ((row * (uint32_t)p.K + 2u * boff) >> p.bs_log2);
       if constexpr (ABL & 1) {
-        q[r] = (uint32_t)b & 255u;
+        q[r] = b & 255u;
         a[r] = 1.0f;
       } else if constexpr (DQ) {
         q[r] = p.sc.qabsmax[b];
@@ -301,8 +315,6 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoa
   }
 };
 
-// The kernel body, for logical workgroup `block` of one GEMV (a plain launch
-// passes blockIdx.x; a grouped launch passes the block index within its segment).
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
   const GemvParams p = load_params(p_in);
@@ -621,7 +633,9 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   p->bs_log2 = bsl;
   p->bs2_log2 = bs2l;
   *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
-            (reinterpret_cast<uintptr_t>(x) % 16) == 0;
+            (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
+            (long long)M * K + 2LL * 1024 < (1LL << 32) &&            // 32-bit element offsets
+            block_base + (long long)M * K / blocksize < (1LL << 32);   // 32-bit block indices
   return QZ_OK;
 }
 

@@ -119,6 +119,15 @@ __global__ __launch_bounds__(T) void k_read_floor_store(const unsigned char *__r
   if ((threadIdx.x & 63) < 2) out[(blockIdx.x * T + threadIdx.x) / 32] = acc;  // 2 rows' worth per wave
 }
 
+// random packed weights (a constant fill would make every LDS lookup a broadcast)
+__global__ void k_fill_random(uint32_t *p, long long n, uint32_t seed) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 0x9E3779B1u ^ seed;
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    p[i] = h;
+  }
+}
+
 int main(int argc, char **argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, K = argc > 2 ? atoi(argv[2]) : 4096;
   const int NC = 64, ITERS = 100;
@@ -128,7 +137,9 @@ int main(int argc, char **argv) {
   for (int i = 0; i < NC; ++i) {
     CK(hipMalloc(&P[i], pbytes)); CK(hipMalloc(&Q[i], nb)); CK(hipMalloc(&A2[i], (nb / 256 + 1) * 4));
     CK(hipMalloc(&A[i], nb * 4));
-    CK(hipMemset(P[i], 0x5A + i, pbytes)); CK(hipMemset(Q[i], 0x40, nb));
+    hipLaunchKernelGGL(k_fill_random, dim3(1024), dim3(256), 0, 0, reinterpret_cast<uint32_t *>(P[i]),
+                       (long long)(pbytes / 4), 0x1234u + i);
+    CK(hipMemset(Q[i], 0x40, nb));
     CK(hipMemset(A2[i], 0x3C, (nb / 256 + 1) * 4)); CK(hipMemset(A[i], 0x3C, nb * 4));
   }
   float *code2, *off; void *x, *y; uint32_t *sink;
@@ -156,12 +167,28 @@ int main(int argc, char **argv) {
   p.sc = ScaleSrc{nullptr, nullptr, nullptr, code2, off, 256};
   p.x = x; p.y = y; p.M = M; p.K = K; p.bs_log2 = 6; p.bs2_log2 = 8; p.lut = nullptr; p.bias = nullptr;
   build_tables(kModeLUT16, QZ_NF4, p.tab, &p.out_scale);
-#define GVN(MODE, DQ, R, WK, NW) timeit("gemv mode=" #MODE " dq=" #DQ " R=" #R " WK=" #WK " NW=" #NW, [&](int i) { \
-    GemvParams q = p; q.B = P[i % NC]; \
+#define GVN(MODE, DQ, R, WK, NW) timeit("gemv mode=" #MODE " dq=" #DQ " R=" #R " WK=" #WK " NW=" #NW, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; \
     if (DQ) { q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; } else { q.sc.absmax = A[i % NC]; } \
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW>), dim3(g), dim3(NW * 64), 0, 0, q); })
 #define GV(MODE, DQ, R, WK) GVN(MODE, DQ, R, WK, 4)
+  // full-control variant: x staged in LDS (XL) and ablation bits (ABL: 1 no scale loads,
+  // 2 no x loads, 4 no reduction/store)
+#define GVF(MODE, DQ, R, WK, NW, XL, ABL) timeit("gemvF mode=" #MODE " R=" #R " WK=" #WK " NW=" #NW " XL=" #XL " ABL=" #ABL, [&](int i) { \
+    GemvParams q = p; q.B = P[i % NC]; \
+    if (DQ) { q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; } else { q.sc.absmax = A[i % NC]; } \
+    const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, XL, ABL>), dim3(g), dim3(NW * 64), XL ? K * 2 : 0, 0, q); })
+  const bool ablate = argc > 4 && std::string(argv[4]) == "ablate";
+  if (ablate) {
+    GV(1, true, 4, 2); GV(1, true, 2, 1); GV(0, true, 4, 2); GV(2, true, 4, 2);
+    GVF(1, true, 4, 2, 4, false, 1); GVF(1, true, 4, 2, 4, false, 2); GVF(1, true, 4, 2, 4, false, 3);
+    GVF(2, true, 4, 2, 4, false, 3); GVF(1, true, 4, 2, 4, true, 0); GVF(1, true, 2, 1, 4, true, 0);
+    GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
+    GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
+  }
+  if (!ablate) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
@@ -181,6 +208,7 @@ int main(int argc, char **argv) {
   if (nsw == 4) { SL(0, 2, 4); SL(0, 4, 4); }
   if (nsw == 7) { SL(0, 2, 7); SL(0, 4, 7); }
   if (nsw == 14) { SL(0, 2, 14); SL(0, 4, 14); }
+  }
   const int ROUNDS = argc > 3 ? atoi(argv[3]) : 9;
   for (auto &v : vs) { for (int i = 0; i < NC; ++i) v.launch(i); }
   CK(hipDeviceSynchronize());

@@ -229,7 +229,7 @@ def prefill_bench(T: int = 16384, iters: int = 10):
             x = x.contiguous()
 
         def fused():
-            return gemm_4bit(x, packed, qs)
+            return gemm_4bit(x, packed, qs, route="fused")
 
         def ref_route():
             return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
@@ -252,10 +252,9 @@ def prefill_bench(T: int = 16384, iters: int = 10):
 
 
 @torch.inference_mode()
-def prefill_sweep(Ts=(16, 64, 256, 1024, 2048, 4096, 16384), iters=10):
+def prefill_sweep(Ts=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 16384), iters=20):
     """4096x4096 NF4: fused MFMA GEMM vs dequant + library GEMM over token count T."""
-    from quantizations_amd import _lib
-    from quantizations_amd.core import dequantize_4bit, quantize_4bit
+    from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
 
     dev = torch.device("cuda")
     torch.manual_seed(12)
@@ -265,11 +264,9 @@ def prefill_sweep(Ts=(16, 64, 256, 1024, 2048, 4096, 16384), iters=10):
     res = {}
     for T in Ts:
         x = torch.randn(T, K, device=dev, dtype=torch.float16)
-        y = torch.empty(T, M, device=dev, dtype=torch.float16)
 
         def fused():
-            _lib.check(_lib.lib.qz_gemm_4bit(T, M, K, x.data_ptr(), K, _lib.DT_F16, packed.data_ptr(), _lib.NF4, 64,
-                                             *qs.scale_args(), 0, y.data_ptr(), M, _lib.stream_of(x)), "gemm")
+            return gemm_4bit(x, packed, qs, route="fused")
 
         def ref_route():
             return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
@@ -279,6 +276,7 @@ def prefill_sweep(Ts=(16, 64, 256, 1024, 2048, 4096, 16384), iters=10):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(50_000_000)  # host enqueues every launch before the GPU reaches them
             e0.record()
             for _ in range(iters):
                 fn()

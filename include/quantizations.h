@@ -132,13 +132,22 @@ int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const voi
                          int blocksize, int blocksize2, const float *lut, void *stream);
 
 /* Fused 4-bit GEMM (prefill, modules.py:62-64): Y[T,M] = X[T,K] . W[M,K]^T
- * (+ bias) with W dequantised tile-by-tile into LDS and multiplied on MFMA
- * (fp16/bf16 in, fp32 accumulate).  X/Y/bias share `dtype` (F16 or BF16);
- * ldx/ldy are row strides in elements. */
+ * (+ bias).  W is decoded tile-by-tile into LDS as exactly the values
+ * qz_dequantize_4bit would store (fp16/bf16 of code * absmax) and multiplied
+ * on MFMA with fp32 accumulation.  X/Y/bias share `dtype` (F16 or BF16);
+ * ldx/ldy are row strides in elements.  Requires K % 64 == 0, M % 4 == 0,
+ * blocksize >= 64 (else QZ_ERR_SHAPE / QZ_ERR_BLOCKSIZE).  For small T the K
+ * range is split across workgroups: pass a workspace of
+ * qz_gemm_4bit_workspace_size(T, M, K) bytes (fp32 partials) to enable it;
+ * with less (or none) the split is reduced accordingly. */
 int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dtype, const unsigned char *B, int quant_type,
                  int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
                  const float *code2, const float *offset, int blocksize2, const void *bias, void *Y, int ldy,
-                 void *stream);
+                 float *workspace, long long workspace_bytes, void *stream);
+
+/* Workspace bytes qz_gemm_4bit uses for (T, M, K) at its preferred K split
+ * (0 = no split). */
+long long qz_gemm_4bit_workspace_size(int T, int M, int K);
 
 /* 4-bit blockwise quantisation (quantize_4bit, core.py:507-559): A[n] of
  * `a_dtype` -> packed out[(n+1)/2] + fp32 absmax[ceil(n/blocksize)]. */

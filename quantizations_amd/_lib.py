@@ -55,7 +55,8 @@ SIGNATURES = {
     "cdequantize_blockwise_fp32_stream": [_p, _p, _p, _p, _i, _i, _p],
     "qz_gemv_4bit": [_i, _i, _p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _ll, _p, _p, _p, _p],
     "qz_gemv_4bit_grouped": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p],
-    "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p],
+    "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p, _ll, _p],
+    "qz_gemm_4bit_workspace_size": [_i, _i, _i],
     "qz_quantize_4bit": [_p, _i, _ll, _i, _i, _p, _p, _p],
     "qz_absmax_mean_workspace": [_ll],
     "qz_absmax_mean": [_p, _ll, _p, _p, _p],
@@ -64,7 +65,7 @@ SIGNATURES = {
     "qz_dequantize_4bit": [_p, _ll, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p],
     "qz_version": [],
 }
-RESTYPES = {"qz_absmax_mean_workspace": _ll}
+RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll}
 
 
 def _load():

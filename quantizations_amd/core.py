@@ -22,6 +22,7 @@ What differs, on purpose (DESIGN.md "Host layer"):
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -379,23 +380,49 @@ def gemv_4bit_grouped(A: Tensor, items) -> list:
     return outs
 
 
-def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = None) -> Tensor:
-    """Batched (prefill) 4-bit GEMM: A[..., K] . W^T -> [..., M] on the fused MFMA
-    kernel when supported (fp16, K % 64 == 0), otherwise the reference's route
-    (dequantize_4bit + torch GEMM)."""
+# Prefill route (matmul_4bit with more than one token).  "fused": the MFMA
+# kernel qz_gemm_4bit (dequant in LDS, never in HBM); "dequant": the
+# reference's own route -- full-weight dequantize_4bit (our HIP kernel) then a
+# library GEMM (hipBLASLt).  "auto" takes the fused kernel up to
+# PREFILL_FUSED_MAX_TOKENS tokens (DESIGN.md section 5 has the measured
+# crossover) and the dequant route above it.
+PREFILL_FUSED_MAX_TOKENS = int(os.environ.get("QZ_PREFILL_FUSED_MAX_T", "512"))
+
+
+def _gemm_fused_ok(A2: Tensor, state: QuantState, M: int, K: int) -> bool:
+    return (A2.dtype in (torch.float16, torch.bfloat16) and K % 64 == 0 and M % 4 == 0
+            and state.blocksize >= 64 and A2.stride(0) % 8 == 0 and A2.data_ptr() % 16 == 0)
+
+
+def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = None, route: str = "auto") -> Tensor:
+    """Batched (prefill) 4-bit GEMM: A[..., K] . W^T (+ bias) -> [..., M].
+
+    The fused MFMA kernel decodes W to exactly the values dequantize_4bit(B,
+    state, out_dtype=A.dtype) stores, so both routes multiply the same operand
+    and differ only in fp32 summation order (fp16/bf16 activations; other
+    dtypes take the dequant route)."""
+    if route not in ("auto", "fused", "dequant"):
+        raise ValueError(f"route must be 'auto', 'fused' or 'dequant', got {route!r}")
     M, K = state.shape[0], state.shape[1]
     lead = A.shape[:-1]
     A2 = A.reshape(-1, K)
     if A2.stride(-1) != 1 or A2.data_ptr() % 16 != 0:
         A2 = A2.contiguous()
     T = A2.shape[0]
-    if A.dtype == torch.float16 and K % 64 == 0 and state.blocksize % 64 == 0 and A2.stride(0) % 8 == 0:
+    fused_ok = _gemm_fused_ok(A2, state, M, K)
+    if route == "fused" and not fused_ok:
+        raise ValueError("gemm_4bit: the fused kernel needs fp16/bf16 activations, K % 64 == 0, M % 4 == 0 "
+                         "and blocksize >= 64")
+    if fused_ok and (route == "fused" or (route == "auto" and T <= PREFILL_FUSED_MAX_TOKENS)):
         out = torch.empty((T, M), dtype=A.dtype, device=A.device)
         if bias is not None and bias.dtype != A.dtype:
             bias = bias.to(A.dtype)
-        check(lib.qz_gemm_4bit(T, M, K, ptr(A2), A2.stride(0), _lib.DT_F16, ptr(B),
+        ws_bytes = int(lib.qz_gemm_4bit_workspace_size(T, M, K))
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=A.device) if ws_bytes > 0 else None
+        check(lib.qz_gemm_4bit(T, M, K, ptr(A2), A2.stride(0), dtype_code(A.dtype), ptr(B),
                                _lib.QUANT_TYPES[state.quant_type], state.blocksize, *state.scale_args(), ptr(bias),
-                               ptr(out), M, _lib.stream_of(A)), "gemm_4bit")
+                               ptr(out), M, ptr(ws), ws_bytes, _lib.stream_of(A)), "gemm_4bit")
         return out.reshape(*lead, M)
-    W = dequantize_4bit(B, state).t()
-    return torch.nn.functional.linear(A, W.to(A.dtype), bias)
+    cd = A.dtype if A.dtype in (torch.float16, torch.bfloat16) else None
+    W = dequantize_4bit(B, state, out_dtype=cd).t()
+    return torch.nn.functional.linear(A, W.to(A.dtype), None if bias is None else bias.to(A.dtype))

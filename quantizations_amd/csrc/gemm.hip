@@ -3,72 +3,118 @@
 // Replaces the reference prefill (modules.py:62-64): a full-weight dequant
 // kernel that writes M*K fp16 to HBM (kernels.cu:554-560), a cast to fp32 and
 // an fp32 SGEMM (F.linear).  Here Y[T, M] = X[T, K] . W[M, K]^T (+ bias) runs
-// in one kernel:
-//   * a 256-thread workgroup owns a 128 (tokens) x 128 (features) output tile
-//     and walks K in steps of 64 -- exactly one scale block (blocksize 64) per
-//     weight row per step;
-//   * the 128 x 64 weight tile arrives as 4 KiB of packed nibbles (16 B per
-//     thread), is decoded in registers to the UNSCALED codebook values in fp16
-//     (v_perm byte tables, as in gemv.hip) and written to LDS; X (128 x 64
-//     fp16) is staged next to it; both images use a 16-B-chunk XOR swizzle so
-//     the ds_read_b128 operand fetches are conflict-free;
-//   * each wave computes 64 x 64 with v_mfma_f32_16x16x32_f16 into a per-step
-//     accumulator, and the step result is folded into the running fp32 sum
-//     with one FMA by the per-column (weight row) scale of that step -- the
-//     block absmax (double quant rebuilt in kernel) times the codebook factor.
-// Requires K % 64 == 0 and blocksize % 64 == 0 (every Llama shape); other
-// shapes return QZ_ERR_SHAPE and the host falls back to dequant + GEMM.
+// in one kernel (plus a tiny reduce kernel when K is split):
+//
+//   * A 256-thread workgroup owns a BT (tokens: 64 or 128) x 128 (weight rows)
+//     output tile and walks its K range in steps of 64 = one scale block per
+//     weight row (blocksize >= 64).
+//   * The W operand is BIT-IDENTICAL to the reference's dequantised fp16/bf16
+//     weight (dequantize_4bit, kernels.cu:554-560 -> our k_dequantize_4bit):
+//     each thread owns 32 codes of one (row, block) and first builds that
+//     block's 16-entry table fp16(code[i] * absmax) (fp32 product, RNE store;
+//     FP4 negatives by sign flip, so code 8 is -0.0 as in the tree), then
+//     decodes its nibbles through the table with the AND-combined v_perm
+//     lookups of gemv.hip.  The GEMM therefore differs from "dequantise, then
+//     fp32 GEMM" only in fp32 summation order.
+//   * Software pipeline: the next K-step's X and W bytes are loaded into
+//     registers before this step's MFMAs; after them the registers are decoded
+//     into the other half of a double-buffered LDS image.  One barrier per step.
+//   * Within every 16-byte (8-element) chunk both operands are stored in the
+//     pair order (e0,e2),(e4,e6),(e1,e3),(e5,e7) that the decode produces; the
+//     dot product over K is order-free, so W needs no re-interleave.
+//   * LDS images are [row][64 elements] with a 16-B-chunk XOR swizzle so the
+//     ds_read_b128 operand fetches are conflict-free.
+//   * v_mfma_f32_16x16x32_{f16,bf16}, fp32 accumulation straight in the MFMA
+//     accumulators (no per-block fold: the scale is inside W).
+//   * Small T: the K range is split over gridDim.z workgroups that write fp32
+//     partial tiles to a caller-provided workspace; k_gemm_reduce sums them
+//     (+ bias) into Y.  The library never allocates.
+// Requires K % 64 == 0, blocksize >= 64 (every Llama shape); other shapes
+// return QZ_ERR_SHAPE and the host falls back to dequantize + library GEMM.
 #include "common.h"
 
 namespace qz {
 
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 b8_t __attribute__((ext_vector_type(8)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-constexpr int kBT = 128, kBM = 128, kBK = 64;
+constexpr int kBM = 128, kBK = 64;
 
 __device__ __forceinline__ uint32_t gperm(uint32_t s0, uint32_t s1, uint32_t sel) {
   return __builtin_amdgcn_perm(s0, s1, sel);
 }
 
-// 8 nibbles -> 4 natural-order half2 (e_2j, e_2j+1) of the unscaled codebook
-// (FP4: values x12, exact; 16-entry: fp16 of the codebook).
-template <int QT>
-__device__ __forceinline__ void decode_nat(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
-  if constexpr (QT == QZ_FP4) {
-    const uint32_t hh = gperm(t[1], t[0], (w >> 4) & 0x07070707u) | (w & 0x80808080u);
-    const uint32_t hl = gperm(t[1], t[0], w & 0x07070707u) | ((w << 4) & 0x80808080u);
-    P[0] = gperm(hh, hl, 0x000C040Cu);
-    P[1] = gperm(hh, hl, 0x010C050Cu);
-    P[2] = gperm(hh, hl, 0x020C060Cu);
-    P[3] = gperm(hh, hl, 0x030C070Cu);
+// fp32 pair -> packed 16-bit pair, round-to-nearest-even (bit-exact with the
+// dequant kernel's stores; see common.h on the scalar-convert tie bug)
+template <int DT> __device__ __forceinline__ uint32_t cvt_pk16(float lo, float hi) {
+  if constexpr (DT == QZ_DT_F16) {
+    return cvt_pk_f16_rne(lo, hi);
   } else {
-    // AND-combined 8-entry lookups (see decode_lut16 in gemv.hip)
-    uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);
-    asm("" : "+v"(ah));
-    const uint32_t bh = ah ^ 0x88888888u;
-    const uint32_t lh = gperm(t[1], t[0], ah) & gperm(t[3], t[2], bh);
-    const uint32_t hh = gperm(t[5], t[4], ah) & gperm(t[7], t[6], bh);
-    uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);
-    asm("" : "+v"(al));
-    const uint32_t bl = al ^ 0x88888888u;
-    const uint32_t ll = gperm(t[1], t[0], al) & gperm(t[3], t[2], bl);
-    const uint32_t hl = gperm(t[5], t[4], al) & gperm(t[7], t[6], bl);
-    const uint32_t q0 = gperm(hh, lh, 0x05010400u);  // (e0, e2)
-    const uint32_t q1 = gperm(hh, lh, 0x07030602u);  // (e4, e6)
-    const uint32_t q2 = gperm(hl, ll, 0x05010400u);  // (e1, e3)
-    const uint32_t q3 = gperm(hl, ll, 0x07030602u);  // (e5, e7)
-    P[0] = gperm(q2, q0, 0x05040100u);               // (e0, e1)
-    P[1] = gperm(q2, q0, 0x07060302u);               // (e2, e3)
-    P[2] = gperm(q3, q1, 0x05040100u);               // (e4, e5)
-    P[3] = gperm(q3, q1, 0x07060302u);               // (e6, e7)
+    uint32_t r;
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+    return r;
   }
 }
 
-// LDS image: [row][64 halfs] = 128-B rows; 16-B chunk c of row r is stored
-// at chunk position c ^ ((r >> 1) & 7): the 16 rows one ds_read_b128 lane
-// group touches land on 16 distinct 16-B bank slots.
+// fp32 FP4 dequant-tree magnitudes (kernels.cu:70-111; sign = bit 3); NF4 uses
+// kNF4 (kernels.cu:851) from common.h
+__device__ __constant__ static const float kFP4Mag[8] = {0.00000000f, 5.208333333e-03f, 0.66666667f, 1.00000000f,
+                                                         0.33333333f, 0.50000000f,      0.16666667f, 0.25000000f};
+
+// 16-entry table of one (row, block): entries fp16/bf16(code[i] * am) as byte
+// planes t[0..3] = low bytes of entries 0-3, 4-7, 8-11, 12-15 and t[4..7] =
+// high bytes (the layout decode_codes expects).
+template <int QT, int DT>
+__device__ __forceinline__ void block_table(float am, uint32_t (&t)[8]) {
+  uint32_t p[8];  // p[k] = (entry 2k, entry 2k+1)
+  if constexpr (QT == QZ_NF4) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = cvt_pk16<DT>(__fmul_rn(kNF4[2 * k], am), __fmul_rn(kNF4[2 * k + 1], am));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p[k] = cvt_pk16<DT>(__fmul_rn(kFP4Mag[2 * k], am), __fmul_rn(kFP4Mag[2 * k + 1], am));
+      p[4 + k] = p[k] ^ 0x80008000u;  // (c * am) * -1: exact sign flip, code 8 -> -0.0
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[j] = gperm(p[2 * j + 1], p[2 * j], 0x06040200u);
+    t[4 + j] = gperm(p[2 * j + 1], p[2 * j], 0x07050301u);
+  }
+}
+
+// 8 nibbles (one dword, high nibble = even element) -> 4 packed 16-bit pairs in
+// the order (e0,e2),(e4,e6),(e1,e3),(e5,e7): AND-combined 8-entry v_perm
+// lookups (see decode_lut16 in gemv.hip).
+__device__ __forceinline__ void decode_codes(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
+  uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);
+  asm("" : "+v"(ah));
+  const uint32_t bh = ah ^ 0x88888888u;
+  const uint32_t lh = gperm(t[1], t[0], ah) & gperm(t[3], t[2], bh);
+  const uint32_t hh = gperm(t[5], t[4], ah) & gperm(t[7], t[6], bh);
+  uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);
+  asm("" : "+v"(al));
+  const uint32_t bl = al ^ 0x88888888u;
+  const uint32_t ll = gperm(t[1], t[0], al) & gperm(t[3], t[2], bl);
+  const uint32_t hl = gperm(t[5], t[4], al) & gperm(t[7], t[6], bl);
+  P[0] = gperm(hh, lh, 0x05010400u);
+  P[1] = gperm(hh, lh, 0x07030602u);
+  P[2] = gperm(hl, ll, 0x05010400u);
+  P[3] = gperm(hl, ll, 0x07030602u);
+}
+
+// natural 8-element chunk (x0..x7 as 4 pairs) -> (x0,x2),(x4,x6),(x1,x3),(x5,x7)
+__device__ __forceinline__ v4u pair_order(const v4u r) {
+  return v4u{gperm(r.y, r.x, 0x05040100u), gperm(r.w, r.z, 0x05040100u), gperm(r.y, r.x, 0x07060302u),
+             gperm(r.w, r.z, 0x07060302u)};
+}
+
+// LDS image: [row][64 elements] = 128-B rows; 16-B chunk c of row r lives at
+// chunk position c ^ ((r >> 1) & 7): the 16 rows one ds_read_b128 lane group
+// touches land on distinct 16-B bank slots.
 __device__ __forceinline__ int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
 struct GemmParams {
@@ -77,162 +123,176 @@ struct GemmParams {
   ScaleSrc sc;
   const void *bias;
   void *Y;
+  float *ws;          // split-K partials [nsplit][T][M] fp32, or nullptr
   int T, M, K, ldx, ldy;
   int bs_log2, bs2_log2;
-  float lut_scale;
-  uint32_t tab[8];
+  int k_split;        // K elements per split (multiple of 64)
 };
 
-template <int QT, bool DQ>
-__global__ __launch_bounds__(256) void k_gemm_4bit_f16(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_x[kBT * 128];
-  __shared__ __attribute__((aligned(16))) unsigned char s_w[kBM * 128];
-  __shared__ float s_scale[kBM];
+template <int QT, bool DQ, int DT, int BT>
+__global__ __launch_bounds__(256) void k_gemm_4bit(GemmParams p) {
+  constexpr int WT = BT / 64;       // waves along T (1 or 2)
+  constexpr int WM = 4 / WT;        // waves along M (4 or 2)
+  constexpr int TI = 4;             // 16-token fragments per wave (64 tokens)
+  constexpr int MJ = kBM / WM / 16; // 16-row fragments per wave (2 or 4)
+  constexpr int XC = BT / 32;       // 16-B X chunks per thread per step
+  __shared__ __attribute__((aligned(16))) unsigned char s_x[2][BT * 128];
+  __shared__ __attribute__((aligned(16))) unsigned char s_w[2][kBM * 128];
   __shared__ float s_code2[DQ ? 256 : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wt = wave >> 1, wm = wave & 1;
-  const int t0 = blockIdx.y * kBT;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave / WM, wm = wave % WM;
   const int m0 = blockIdx.x * kBM;
-  const int row_bytes = p.K >> 1;
+  const int t0 = blockIdx.y * BT;
+  const int kbeg = blockIdx.z * p.k_split;
+  const int kend = min(p.K, kbeg + p.k_split);
+  const int nsteps = (kend - kbeg) / kBK;
+  const uint32_t row_bytes = (uint32_t)p.K >> 1;
 
   float offset = 0.0f;
   if constexpr (DQ) {
     s_code2[tid] = p.sc.code2[tid];
     offset = *p.sc.offset;
   }
-  uint32_t tab[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) tab[i] = p.tab[i];
 
-  f4_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
-
-  // weight-tile ownership: thread -> (row wr, 32-element half wh)
+  // weight ownership: thread -> (row wr, 32-code half wh of the 64-code step)
   const int wr = tid >> 1, wh = tid & 1;
-  const int wrow = m0 + wr;
-  const bool wrow_ok = wrow < p.M;
-  const int fr = lane & 15, fk = lane >> 4;  // MFMA fragment row / k-group
+  const int wrow = min(m0 + wr, p.M - 1);  // clamped: rows >= M are computed and never stored
+  const unsigned char *wptr = p.B + (size_t)wrow * row_bytes + 16 * wh;
+  const uint32_t blk_row = (uint32_t)(((long long)wrow * p.K) >> p.bs_log2);  // K % 64 == 0, blocksize >= 64
 
-  for (int k0 = 0; k0 < p.K; k0 += kBK) {
-    // ---- issue this step's global loads ----
-    v4u xv[4];
+  // ---- staged registers of one K-step ----
+  v4u xv[XC];
+  v4u wv;
+  uint32_t q = 0;
+  float a = 0.0f;
+  auto load_step = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XC; ++i) {
       const int c = tid + 256 * i;
-      const int r = c >> 3, kc = c & 7;
-      const int t = t0 + r;
-      xv[i] = t < p.T ? *reinterpret_cast<const v4u *>(reinterpret_cast<const uint16_t *>(p.X) + (size_t)t * p.ldx +
-                                                       k0 + 8 * kc)
+      const int t = t0 + (c >> 3);
+      xv[i] = t < p.T ? *reinterpret_cast<const v4u *>(reinterpret_cast<const uint16_t *>(p.X) +
+                                                      (size_t)t * p.ldx + k0 + 8 * (c & 7))
                       : v4u{0u, 0u, 0u, 0u};
     }
-    v4u wv = v4u{0u, 0u, 0u, 0u};
-    uint32_t q = 0;
-    float a = 0.0f;
-    if (wrow_ok) {
-      wv = __builtin_nontemporal_load(
-          reinterpret_cast<const v4u *>(p.B + (size_t)wrow * row_bytes + (k0 >> 1) + 16 * wh));
-      const long long b = ((long long)wrow * p.K + k0) >> p.bs_log2;
-      if constexpr (DQ) {
-        q = p.sc.qabsmax[b];
-        a = p.sc.absmax2[b >> p.bs2_log2];
-      } else {
-        a = p.sc.absmax[b];
-      }
+    wv = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(wptr + (k0 >> 1)));
+    const uint32_t b = blk_row + ((uint32_t)k0 >> p.bs_log2);
+    if constexpr (DQ) {
+      q = p.sc.qabsmax[b];
+      a = p.sc.absmax2[b >> p.bs2_log2];
+    } else {
+      a = p.sc.absmax[b];
     }
-    __syncthreads();  // previous step's LDS reads are done; s_code2 staged
-
-    // ---- decode W to LDS, copy X to LDS ----
+  };
+  auto store_step = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < XC; ++i) {
       const int c = tid + 256 * i;
-      *reinterpret_cast<v4u *>(s_x + lds_off(c >> 3, c & 7)) = xv[i];
+      *reinterpret_cast<v4u *>(s_x[buf] + lds_off(c >> 3, c & 7)) = pair_order(xv[i]);
     }
-    {
-      const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+    float am;
+    if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[q], a), offset);  // core.py:467-468
+    else am = a;
+    uint32_t t[8];
+    block_table<QT, DT>(am, t);
+    const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t P[4];
-        decode_nat<QT>(w[d], tab, P);
-        *reinterpret_cast<v4u *>(s_w + lds_off(wr, 4 * wh + d)) = v4u{P[0], P[1], P[2], P[3]};
-      }
-      if (wh == 0) {
-        float am;
-        if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[q], a), offset);
-        else am = a;
-        s_scale[wr] = wrow_ok ? am * p.lut_scale : 0.0f;
-      }
+    for (int d = 0; d < 4; ++d) {
+      uint32_t P[4];
+      decode_codes(w[d], t, P);
+      *reinterpret_cast<v4u *>(s_w[buf] + lds_off(wr, 4 * wh + d)) = v4u{P[0], P[1], P[2], P[3]};
     }
-    __syncthreads();
+  };
 
-    // ---- MFMA: per-step product, then scaled fold into acc ----
-    f4_t part[4][4];
+  f4_t acc[TI][MJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = lane >> 4;  // MFMA fragment row / k-group
+  if (nsteps > 0) {
+    load_step(kbeg);
+    if constexpr (DQ) __syncthreads();  // s_code2 staged
+    store_step(0);
+    __syncthreads();
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) load_step(kbeg + (s + 1) * kBK);  // in flight during this step's MFMAs
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      h8_t af[4], bf[4];
+      v4u af[TI], bf[MJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        af[i] = *reinterpret_cast<const h8_t *>(s_x + lds_off(64 * wt + 16 * i + fr, 4 * kk + fk));
-        bf[i] = *reinterpret_cast<const h8_t *>(s_w + lds_off(64 * wm + 16 * i + fr, 4 * kk + fk));
-      }
+      for (int i = 0; i < TI; ++i)
+        af[i] = *reinterpret_cast<const v4u *>(s_x[cur] + lds_off(64 * wt + 16 * i + fr, 4 * kk + fk));
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < MJ; ++j)
+        bf[j] = *reinterpret_cast<const v4u *>(s_w[cur] + lds_off((kBM / WM) * wm + 16 * j + fr, 4 * kk + fk));
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          part[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], kk == 0 ? f4_t{0.f, 0.f, 0.f, 0.f}
-                                                                                    : part[i][j], 0, 0, 0);
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) {
+          if constexpr (DT == QZ_DT_F16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, af[i]),
+                                                               __builtin_bit_cast(h8_t, bf[j]), acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, af[i]),
+                                                                __builtin_bit_cast(b8_t, bf[j]), acc[i][j], 0, 0, 0);
+        }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float sc = s_scale[64 * wm + 16 * j + fr];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = fmaf(part[i][j][r], sc, acc[i][j][r]);
-    }
+    if (more) store_step(cur ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
   }
 
-  // ---- epilogue: C/D map col = lane & 15, row = 4 * (lane >> 4) + r ----
+  // ---- epilogue: C/D map col (weight row) = lane & 15, row (token) = 4 * (lane >> 4) + r ----
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = m0 + 64 * wm + 16 * j + fr;
+  for (int j = 0; j < MJ; ++j) {
+    const int m = m0 + (kBM / WM) * wm + 16 * j + fr;
     if (m >= p.M) continue;
-    const float bv = p.bias ? __half2float(reinterpret_cast<const __half *>(p.bias)[m]) : 0.0f;
+    if (p.ws) {  // split-K partial
+      float *ws = p.ws + (size_t)blockIdx.z * p.T * p.M;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = t0 + 64 * wt + 16 * i + 4 * fk + r;
+          if (t < p.T) ws[(size_t)t * p.M + m] = acc[i][j][r];
+        }
+      continue;
+    }
+    const float bv = p.bias ? load_f32<DT>(p.bias, m) : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = t0 + 64 * wt + 16 * i + 4 * fk + r;
-        if (t < p.T)
-          reinterpret_cast<uint16_t *>(p.Y)[(size_t)t * p.ldy + m] = f32_to_f16_bits(acc[i][j][r] + bv);
+        if (t < p.T) store_f32<DT>(p.Y, (long long)t * p.ldy + m, acc[i][j][r] + bv);
       }
   }
 }
 
-static void gemm_tables(int quant_type, uint32_t tab[8], float *lut_scale) {
-  for (int i = 0; i < 8; ++i) tab[i] = 0;
-  if (quant_type == QZ_FP4) {
-    const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};  // fp16 hi bytes of {0,1/16,8,12,4,6,2,3}
-    for (int i = 0; i < 8; ++i) tab[i >> 2] |= (uint32_t)hb[i] << (8 * (i & 3));
-    *lut_scale = 1.0f / 12.0f;
-    return;
+// Y[t, m] = sum_z ws[z][t][m] (+ bias[m]); 4 consecutive m per thread.
+template <int DT>
+__global__ __launch_bounds__(256) void k_gemm_reduce(const float *__restrict__ ws, int nsplit, int T, int M,
+                                                     const void *bias, void *Y, int ldy) {
+  const long long i4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long long n = (long long)T * M;
+  if (i4 >= n) return;
+  const int t = (int)(i4 / M), m = (int)(i4 % M);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < nsplit; ++z) {
+    const float4 v = *reinterpret_cast<const float4 *>(ws + (size_t)z * n + i4);
+    s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
   }
-  static const float nf4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
-                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
-                                0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
-                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-                                0.7229568362236023f, 1.0f};
-  for (int i = 0; i < 16; ++i) {
-    const uint16_t h = __half_as_ushort(__float2half_rn(nf4[i]));
-    tab[i >> 2] |= (uint32_t)(h & 0xFF) << (8 * (i & 3));
-    tab[4 + (i >> 2)] |= (uint32_t)(h >> 8) << (8 * (i & 3));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float b = bias ? load_f32<DT>(bias, m + j) : 0.0f;
+    store_f32<DT>(Y, (long long)t * ldy + m + j, s[j] + b);
   }
-  *lut_scale = 1.0f;
 }
 
 static int ilog2g(long long v) {
@@ -241,26 +301,52 @@ static int ilog2g(long long v) {
   return (1LL << l) == v ? l : -1;
 }
 
+// Tile / split choice: BT = 64 tokens for T <= 64, else 128; K is split over
+// up to 16 workgroups (>= 4 K-steps each) until the grid has >= 512 workgroups
+// (2 per CU), as long as the fp32 partials fit the caller's workspace.
+static void gemm_plan(int T, int M, int K, long long ws_bytes, int *bt, int *nsplit, int *k_split) {
+  *bt = T <= 64 ? 64 : 128;
+  const long long tiles = (long long)((M + kBM - 1) / kBM) * ((T + *bt - 1) / *bt);
+  const int steps = K / kBK;
+  int s = 1;
+  while (tiles * s < 512 && s * 2 <= 16 && steps / (s * 2) >= 4 &&
+         (long long)(s * 2) * T * M * 4 <= ws_bytes)
+    s *= 2;
+  const int per = (steps + s - 1) / s;
+  *nsplit = (steps + per - 1) / per;
+  *k_split = per * kBK;
+}
+
 }  // namespace qz
 
 using namespace qz;
 
+extern "C" long long qz_gemm_4bit_workspace_size(int T, int M, int K) {
+  if (T <= 0 || M <= 0 || K <= 0 || K % kBK != 0) return 0;
+  int bt, ns, ks;
+  gemm_plan(T, M, K, (long long)1 << 62, &bt, &ns, &ks);
+  return ns > 1 ? (long long)ns * T * M * 4 : 0;
+}
+
 extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dtype, const unsigned char *B,
                             int quant_type, int blocksize, const float *absmax, const unsigned char *qabsmax,
                             const float *absmax2, const float *code2, const float *offset, int blocksize2,
-                            const void *bias, void *Y, int ldy, void *stream) {
+                            const void *bias, void *Y, int ldy, float *workspace, long long workspace_bytes,
+                            void *stream) {
   if (!X || !B || !Y || T < 0 || M < 0 || K < 0) return QZ_ERR_ARG;
   if ((absmax == nullptr) == (qabsmax == nullptr)) return QZ_ERR_ARG;
   const bool dq = qabsmax != nullptr;
   if (dq && (!absmax2 || !code2 || !offset)) return QZ_ERR_ARG;
   if (quant_type != QZ_FP4 && quant_type != QZ_NF4) return QZ_ERR_DTYPE;
-  if (dtype != QZ_DT_F16) return QZ_ERR_DTYPE;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_DTYPE;
   const int bsl = ilog2g(blocksize), bs2l = dq ? ilog2g(blocksize2) : 0;
   if (bsl < 6 || bs2l < 0) return QZ_ERR_BLOCKSIZE;
-  if (K % kBK != 0 || ldx < K || ldy < M || (ldx % 8) != 0 ||
-      (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(B) % 16) != 0)
+  if (K % kBK != 0 || ldx < K || ldy < M || (ldx % 8) != 0 || (M % 4) != 0 ||
+      (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(B) % 16) != 0 ||
+      (long long)M * K / blocksize >= (1LL << 32))
     return QZ_ERR_SHAPE;
   if (T == 0 || M == 0) return QZ_OK;
+  if (workspace_bytes < 0 || (workspace_bytes > 0 && !workspace)) return QZ_ERR_ARG;
   GemmParams p;
   p.X = X;
   p.B = B;
@@ -274,16 +360,33 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
   p.ldy = ldy;
   p.bs_log2 = bsl;
   p.bs2_log2 = bs2l;
-  gemm_tables(quant_type, p.tab, &p.lut_scale);
-  const dim3 grid((unsigned)((M + kBM - 1) / kBM), (unsigned)((T + kBT - 1) / kBT));
+  int bt, nsplit;
+  gemm_plan(T, M, K, workspace ? workspace_bytes : 0, &bt, &nsplit, &p.k_split);
+  p.ws = nsplit > 1 ? workspace : nullptr;
+  const dim3 grid((unsigned)((M + kBM - 1) / kBM), (unsigned)((T + bt - 1) / bt), (unsigned)nsplit);
   hipStream_t s = (hipStream_t)stream;
+#define QZ_GEMM(QT_, DQ_, DT_, BT_) hipLaunchKernelGGL((k_gemm_4bit<QT_, DQ_, DT_, BT_>), grid, dim3(256), 0, s, p)
+#define QZ_GEMM_BT(QT_, DQ_, DT_) \
+  do { if (bt == 64) QZ_GEMM(QT_, DQ_, DT_, 64); else QZ_GEMM(QT_, DQ_, DT_, 128); } while (0)
+#define QZ_GEMM_DT(QT_, DQ_) \
+  do { if (dtype == QZ_DT_F16) QZ_GEMM_BT(QT_, DQ_, QZ_DT_F16); else QZ_GEMM_BT(QT_, DQ_, QZ_DT_BF16); } while (0)
   if (quant_type == QZ_FP4) {
-    if (dq) hipLaunchKernelGGL((k_gemm_4bit_f16<QZ_FP4, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_gemm_4bit_f16<QZ_FP4, false>), grid, dim3(256), 0, s, p);
+    if (dq) QZ_GEMM_DT(QZ_FP4, true); else QZ_GEMM_DT(QZ_FP4, false);
   } else {
-    if (dq) hipLaunchKernelGGL((k_gemm_4bit_f16<QZ_NF4, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((k_gemm_4bit_f16<QZ_NF4, false>), grid, dim3(256), 0, s, p);
+    if (dq) QZ_GEMM_DT(QZ_NF4, true); else QZ_GEMM_DT(QZ_NF4, false);
   }
+#undef QZ_GEMM_DT
+#undef QZ_GEMM_BT
+#undef QZ_GEMM
   QZ_LAUNCH_CHECK();
+  if (nsplit > 1) {
+    const long long n4 = ((long long)T * M) / 4;
+    const unsigned g = (unsigned)((n4 + 255) / 256);
+    if (dtype == QZ_DT_F16)
+      hipLaunchKernelGGL((k_gemm_reduce<QZ_DT_F16>), dim3(g), dim3(256), 0, s, workspace, nsplit, T, M, bias, Y, ldy);
+    else
+      hipLaunchKernelGGL((k_gemm_reduce<QZ_DT_BF16>), dim3(g), dim3(256), 0, s, workspace, nsplit, T, M, bias, Y, ldy);
+    QZ_LAUNCH_CHECK();
+  }
   return QZ_OK;
 }

@@ -422,6 +422,83 @@ def test_gemm_bias_and_batch_dims(orc):
     assert_close(Y.reshape(T, M).float().cpu(), Yref, torch.float16, "gemm bias")
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+@pytest.mark.parametrize("dq", [True, False])
+@pytest.mark.parametrize("T,M,K", [(1, 256, 4096), (37, 512, 1024), (64, 4096, 4096), (200, 1024, 2048)])
+def test_gemm_w_operand_is_the_dequantised_weight(qt, dq, dt, T, M, K):
+    """One-hot activations read single weights back through the MFMA path: row t
+    of Y must equal column k_t of dequantize_4bit(W, out_dtype=dt) BIT FOR BIT
+    (values; -0.0 reads back as +0.0).  Pins the in-LDS decode (per-block
+    fp16/bf16 table of code*absmax, double-quant rebuild, pair order shared by
+    X and W) to the dequant kernel; covers both token tiles and split-K."""
+    from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
+
+    W = _w(M, K, seed=3 * T + M)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+    ks = (torch.arange(T) * 997 + 13) % K          # probe positions across blocks and nibble slots
+    X = torch.zeros(T, K, dtype=dt)
+    X[torch.arange(T), ks] = 1.0
+    Y = gemm_4bit(X.to(DEV), packed, st, route="fused")
+    assert Y.shape == (T, M) and Y.dtype == dt
+    Wd = dequantize_4bit(packed, st, out_dtype=dt).t()   # [M, K]
+    assert torch.equal(Y, Wd[:, ks.to(DEV)].t()), f"{qt} dq={dq} {dt} {T}x{M}x{K}"
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("T,M,K", [(5, 512, 1024), (64, 4096, 4096), (300, 768, 4096)])
+def test_gemm_random_activations_vs_fp64(dt, T, M, K):
+    """Random activations: fused result vs an fp64 matmul of the dequantised
+    weight -- only fp32 summation order and the output rounding differ."""
+    from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
+
+    W = _w(M, K, seed=T + 7 * M)
+    X = torch.randn(T, K, generator=torch.Generator().manual_seed(T + K)).to(dt).to(DEV)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    Y = gemm_4bit(X, packed, st, route="fused")
+    ref = X.double() @ dequantize_4bit(packed, st, out_dtype=dt).double()
+    assert_close(Y.float().cpu(), ref.cpu().numpy(), dt, f"gemm vs fp64 {dt} {T}x{M}x{K}")
+
+
+def test_gemm_routes_agree_and_fallbacks():
+    """route='fused' and route='dequant' multiply the same operand; shapes the
+    fused kernel does not take (M % 4 != 0, fp32 input) fall back in 'auto'."""
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    W = _w(512, 1024, seed=1)
+    X = torch.randn(100, 1024, generator=torch.Generator().manual_seed(2)).half().to(DEV)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    a = gemm_4bit(X, packed, st, route="fused").double()
+    b = gemm_4bit(X, packed, st, route="dequant").double()
+    assert ((a - b).norm() / b.norm()) < 2e-3
+    W2 = _w(510, 1024, seed=3)
+    p2, s2 = quantize_4bit(W2.to(DEV), quant_type="nf4")
+    with pytest.raises(ValueError):
+        gemm_4bit(X, p2, s2, route="fused")
+    y2 = gemm_4bit(X, p2, s2)  # auto -> dequant route
+    assert y2.shape == (100, 510)
+    y3 = gemm_4bit(X.float(), packed, st)  # fp32 activations -> dequant route, fp32 out
+    assert y3.dtype == torch.float32 and ((y3.double() - b).norm() / b.norm()) < 2e-3
+
+
+def test_gemm_split_k_with_bias_matches_unsplit(orc):
+    """Small T splits K over workgroups (fp32 partials + reduce kernel): same
+    result as the oracle, bias added once."""
+    from quantizations_amd import _lib
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    T, M, K = 8, 1024, 8192
+    assert _lib.lib.qz_gemm_4bit_workspace_size(T, M, K) > 0  # this shape does split
+    W = _w(M, K, seed=11)
+    X = torch.randn(T, K, generator=torch.Generator().manual_seed(12)).half()
+    bias = torch.randn(M, generator=torch.Generator().manual_seed(13)).half()
+    packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+    Y = gemm_4bit(X.to(DEV), packed, st, bias=bias.to(DEV), route="fused")
+    o = orc.quantize_4bit(W.float().numpy(), 64, "nf4")
+    Yref = (X.double() @ torch.from_numpy(orc.dequantize(o)).double().t() + bias.double()).numpy()
+    assert_close(Y.float().cpu(), Yref, torch.float16, "split-K + bias")
+
+
 # ---------------------------------------------------------------------------
 # module level: Linear4bit drop-in
 # ---------------------------------------------------------------------------

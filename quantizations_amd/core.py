@@ -22,6 +22,7 @@ What differs, on purpose (DESIGN.md "Host layer"):
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 from typing import Optional, Tuple
 
@@ -83,7 +84,14 @@ class QuantState:
                     int(self.state2.blocksize))
         return (ptr(self.absmax), 0, 0, 0, 0, 0)
 
-    # -- serialisation (bnb-compatible key names, reference valid_qs_keys) --
+    # -- serialisation ------------------------------------------------------
+    # Key names are the reference's valid_qs_keys (core.py:29-42), which it
+    # declares but never serialises; the layout is the bitsandbytes one those
+    # names come from, so checkpoints interoperate: tensors under their own
+    # keys, every non-tensor field JSON-encoded into ONE uint8 tensor under
+    # "quant_state.bitsandbytes__<quant_type>" (safetensors holds tensors only).
+    PACKED_PREFIX = "quant_state.bitsandbytes__"
+
     def as_dict(self, packed: bool = False) -> dict:
         d = {
             "quant_type": self.quant_type,
@@ -99,13 +107,33 @@ class QuantState:
                 "nested_blocksize": self.state2.blocksize,
                 "nested_quant_map": self.state2.code,
                 "nested_dtype": str(self.state2.dtype).replace("torch.", ""),
-                "nested_offset": self.offset.item() if self.offset.numel() == 1 else self.offset,
+                "nested_offset": float(self.offset.item()),
             })
-        return d
+        if not packed:
+            return d
+        out = {k: v for k, v in d.items() if isinstance(v, Tensor)}
+        meta = {k: (list(v) if isinstance(v, tuple) else v) for k, v in d.items() if not isinstance(v, Tensor)}
+        out[self.PACKED_PREFIX + self.quant_type] = _pack_json(meta)
+        return out
 
     @classmethod
     def from_dict(cls, qs_dict: dict, device) -> "QuantState":
-        d = dict(qs_dict)
+        """Rebuild from as_dict() output, packed or not.  Keys may carry a
+        module prefix (e.g. "layers.0.q_proj.weight.absmax")."""
+        d = {}
+        for k, v in qs_dict.items():
+            short = k[k.index(cls.PACKED_PREFIX):] if cls.PACKED_PREFIX in k else k.split(".")[-1]
+            d[short] = v
+        packed_keys = [k for k in d if k.startswith(cls.PACKED_PREFIX)]
+        if len(packed_keys) > 1:
+            raise ValueError(f"more than one packed quant_state entry: {packed_keys}")
+        if packed_keys:
+            d.update(_unpack_json(d.pop(packed_keys[0])))
+        missing = [k for k in ("absmax", "quant_map", "quant_type", "blocksize", "dtype", "shape") if k not in d]
+        if missing:
+            raise ValueError(f"quant_state is missing {missing}")
+        if d["quant_type"] not in cls.valid_quant_types:
+            raise ValueError(f"unknown quant_type {d['quant_type']!r}")
         state2 = None
         offset = None
         if "nested_absmax" in d:
@@ -117,6 +145,14 @@ class QuantState:
         return cls(quant_type=d["quant_type"], absmax=d["absmax"].to(device), blocksize=int(d["blocksize"]),
                    code=d["quant_map"].to(device), dtype=getattr(torch, d["dtype"]), shape=torch.Size(d["shape"]),
                    offset=offset, state2=state2)
+
+
+def _pack_json(obj: dict) -> Tensor:
+    return torch.tensor(list(json.dumps(obj, sort_keys=True).encode("utf-8")), dtype=torch.uint8)
+
+
+def _unpack_json(t: Tensor) -> dict:
+    return json.loads(bytes(t.detach().cpu().to(torch.uint8).tolist()).decode("utf-8"))
 
 
 class Params4bit(torch.nn.Parameter):
@@ -136,6 +172,20 @@ class Params4bit(torch.nn.Parameter):
         self.compress_statistics = compress_statistics
         self.data = data
         self.module = module
+        return self
+
+    @classmethod
+    def from_prequantized(cls, data: Tensor, quantized_stats: dict, requires_grad: bool = False, device="cuda",
+                          module=None, **kwargs) -> "Params4bit":
+        """A Params4bit around already-packed bytes and their statistics (the
+        QuantState.as_dict keys, packed or not): loading a pre-quantised
+        checkpoint never re-quantises."""
+        qs = QuantState.from_dict(quantized_stats, device=device)
+        self = cls(data.to(device), requires_grad=requires_grad, quant_state=qs, blocksize=qs.blocksize,
+                   quant_type=qs.quant_type, quant_storage=data.dtype, module=module, bnb_quantized=True,
+                   compress_statistics=qs.nested)
+        if module is not None:
+            module.quant_state = qs
         return self
 
     def _quantize(self, device):

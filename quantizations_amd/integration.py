@@ -15,7 +15,7 @@ from typing import Iterable, Optional
 import torch
 import torch.nn as nn
 
-from .core import Params4bit
+from .core import Params4bit, QuantState
 from .modules import DecodeGroup, Linear4bit, _linear4bit_group_compute
 
 
@@ -121,3 +121,57 @@ def unfuse_projection_groups(model: nn.Module) -> None:
     """Remove every DecodeGroup attached by fuse_projection_groups."""
     for m in model.modules():
         m.__dict__.pop("_qz_group", None)
+
+
+# ---------------------------------------------------------------------------
+# pre-quantised checkpoints (SURVEY.md 8f row 1)
+# ---------------------------------------------------------------------------
+
+def save_quantized(model: nn.Module, path: str) -> None:
+    """Write `model`'s state dict (Linear4bit weights as packed bytes + their
+    quant_state in the bnb key layout) to a safetensors file."""
+    from safetensors.torch import save_file
+
+    sd = {}
+    seen = {}
+    for k, v in model.state_dict().items():
+        t = v.detach().to("cpu").contiguous()
+        key = (t.data_ptr(), t.dtype, tuple(t.shape)) if t.numel() else None
+        if key is not None and key in seen:  # tied tensors: safetensors stores each once
+            t = t.clone()
+        seen[key] = k
+        sd[k] = t
+    save_file(sd, path, metadata={"format": "pt", "quantization": "bitsandbytes-4bit-compatible (quantizations_amd)"})
+
+
+def load_quantized(model: nn.Module, path: str, device=None, modules_to_not_convert: Optional[Iterable[str]] = None,
+                   compute_dtype=None) -> nn.Module:
+    """Load a save_quantized() checkpoint into `model` without re-quantising.
+
+    `model` may be built on the meta device (``with torch.device("meta"):``).
+    Every nn.Linear whose checkpoint entry carries a packed quant_state becomes
+    a Linear4bit around the stored bytes; everything else is assigned as is.
+    The model is then moved to `device` (default "cuda")."""
+    from safetensors.torch import load_file
+
+    sd = load_file(path, device="cpu")
+    marker = "." + QuantState.PACKED_PREFIX
+    quantised = {k[:k.index(marker)] for k in sd if marker in k}   # e.g. "model.layers.0.self_attn.q_proj.weight"
+    skip = set(modules_to_not_convert or [])
+
+    def visit(parent: nn.Module, prefix: str):
+        for name, child in list(parent.named_children()):
+            full = f"{prefix}.{name}" if prefix else name
+            if isinstance(child, nn.Linear) and not isinstance(child, Linear4bit) and \
+                    full + ".weight" in quantised and name not in skip:
+                parent._modules[name] = Linear4bit(child.in_features, child.out_features, child.bias is not None,
+                                                   compute_dtype, device="meta")
+            else:
+                visit(child, full)
+
+    visit(model, "")
+    missing, unexpected = model.load_state_dict(sd, strict=False, assign=True)
+    missing = [k for k in missing if not k.endswith("rotary_emb.inv_freq")]
+    if missing or unexpected:
+        raise RuntimeError(f"load_quantized: missing {missing[:5]}..., unexpected {unexpected[:5]}...")
+    return model.to(device or "cuda")

@@ -119,6 +119,34 @@ class Linear4bit(nn.Linear):
         out = matmul_4bit(xin, self.weight, bias=bias, quant_state=qs)
         return out if out.dtype == inp_dtype else out.to(inp_dtype)
 
+    # -- checkpoints: bnb-compatible keys (QuantState.as_dict(packed=True)) --
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+        qs = self.weight.quant_state
+        if qs is None:
+            return  # not quantised yet: the plain float weight is saved
+        w = self.weight
+        destination[prefix + "weight"] = w if keep_vars else w.data.detach()
+        for k, v in qs.as_dict(packed=True).items():
+            destination[prefix + "weight." + k] = v if keep_vars else v.detach()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        wkey = prefix + "weight"
+        stats = {k[len(wkey) + 1:]: v for k, v in state_dict.items() if k.startswith(wkey + ".")}
+        if not stats or wkey not in state_dict:  # float checkpoint: quantised on .to(cuda)
+            super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                          unexpected_keys, error_msgs)
+            return
+        data = state_dict[wkey]
+        dev = self.weight.device if self.weight.device.type != "meta" else data.device
+        self.weight = Params4bit.from_prequantized(data, stats, requires_grad=False, device=dev, module=self)
+        rest = {k: v for k, v in state_dict.items() if k != wkey and not k.startswith(wkey + ".")}
+        n_missing = len(missing_keys)
+        super()._load_from_state_dict(rest, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                                      error_msgs)
+        missing_keys[n_missing:] = [k for k in missing_keys[n_missing:] if k != wkey]
+
     def dequantize(self) -> torch.Tensor:
         """Dense weight [out, in] in the original dtype (for checks and export)."""
         return dequantize_4bit(self.weight, self.weight.quant_state).t()

@@ -331,6 +331,8 @@ def main():
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
+    ap.add_argument("--force-shard", action="store_true",
+                    help="run the multi-GPU code path (process group, sharded layers, RCCL) even at world size 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -339,7 +341,8 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
-    if world > 1:
+    sharded = world > 1 or args.force_shard
+    if sharded:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     if args.gemv_only:
@@ -357,7 +360,7 @@ def main():
 
     t_build = time.perf_counter()
     model, cfg = build_model(args.layers, seed=0)
-    if world > 1:
+    if sharded:
         from quantizations_amd.parallel import shard_model_linear4bit
         shard_model_linear4bit(model, rank, world)
         torch.cuda.empty_cache()
@@ -421,12 +424,12 @@ def main():
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
                        "prompt_len": args.prompt, "batch": 1, "decode": mode,
-                       "parallelism": "single" if world == 1 else f"rowsplit-tp{world}-allgather",
+                       "parallelism": f"rowsplit-tp{world}-allgather" if sharded else "single",
                        "projection_groups": n_groups},
             "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -11,10 +11,12 @@ config #1 CPU dequant+matmul baseline.
   fp16 (transformers' default skip list).  A step = one generated token
   (full forward: embeddings, 32 layers with attention + KV cache, lm_head,
   argmax).  value = generated tokens / s.
-* N > 1 (torchrun, one process per GPU): every Linear4bit is row-sharded
-  (rows p*M/N..(p+1)*M/N on rank p, sliced from the global quant state) and
-  its output all-gathered over RCCL; the same single decode stream is served
-  by all N GPUs (strong scaling).
+* N > 1 (torchrun, one process per GPU), default --tp-mode pair: Megatron
+  pairing -- q/k/v and gate/up column-parallel (rank p keeps its heads / MLP
+  columns as row slices of the global quant state), o_proj and down_proj
+  row-parallel (input-column slices) + one RCCL all-reduce each: 2 collectives
+  per layer.  --tp-mode gather: every Linear4bit row-split + all-gather.  The
+  same single decode stream is served by all N GPUs (strong scaling).
 * roofline: the 4096x4096 NF4+DQ fused GEMV alone, 64 rotating weight copies
   (> the 256 MiB Infinity Cache), HIP events on the launch stream around 400
   back-to-back launches (average launch duration, matches rocprofv3);
@@ -331,6 +333,9 @@ def main():
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
+    ap.add_argument("--tp-mode", choices=("pair", "gather"), default="pair",
+                    help="multi-GPU layout: Megatron pairing (column q/k/v/gate/up + row o/down, 2 all-reduces per "
+                         "layer) or row-split every Linear4bit + all-gather")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the multi-GPU code path (process group, sharded layers, RCCL) even at world size 1")
     args = ap.parse_args()
@@ -361,8 +366,14 @@ def main():
     t_build = time.perf_counter()
     model, cfg = build_model(args.layers, seed=0)
     if sharded:
-        from quantizations_amd.parallel import shard_model_linear4bit
-        shard_model_linear4bit(model, rank, world)
+        if args.tp_mode == "pair":
+            from quantizations_amd.parallel import apply_tensor_parallel
+            apply_tensor_parallel(model, rank, world)
+        else:
+            from quantizations_amd.parallel import shard_model_linear4bit
+            shard_model_linear4bit(model, rank, world)
+        import gc
+        gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
         torch.cuda.empty_cache()
     n_groups = 0
     if not args.no_fuse:
@@ -424,7 +435,9 @@ def main():
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
                        "prompt_len": args.prompt, "batch": 1, "decode": mode,
-                       "parallelism": f"rowsplit-tp{world}-allgather" if sharded else "single",
+                       "parallelism": ("single" if not sharded else
+                                       f"tp{world}-megatron-pair-allreduce" if args.tp_mode == "pair" else
+                                       f"tp{world}-rowsplit-allgather"),
                        "projection_groups": n_groups},
             "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
         }

@@ -82,7 +82,7 @@ def _group_compatible(members) -> bool:
             return False
     elif cls is RowShardedLinear4bit:
         states = [m.state for m in members]
-        if len({(m.world_size, id(m.group)) for m in members}) != 1 or \
+        if len({(m.world_size, id(m.group), m.gather) for m in members}) != 1 or \
                 any(m._local_matmul is not members[0]._local_matmul for m in members):
             return False
     else:

@@ -71,8 +71,9 @@ class RowShardedLinear4bit(nn.Module):
     output on every rank: local fused 4-bit matmul, then an all-gather."""
 
     def __init__(self, full: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 group=None, local_matmul: Optional[Callable] = None):
+                 group=None, local_matmul: Optional[Callable] = None, gather: bool = True):
         super().__init__()
+        self.gather = gather  # False: column-parallel (Megatron), the output stays this rank's shard
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world_size = dist.get_world_size(group) if world_size is None else world_size
         self.group = group
@@ -108,6 +109,8 @@ class RowShardedLinear4bit(nn.Module):
         if group is not None and x.numel() == x.shape[-1]:
             return group.take(self, x)
         y = self.local_forward(x)                       # [..., M/P]
+        if not self.gather:
+            return y
         lead = y.shape[:-1]
         rows = y.shape[-1]
         y2 = y.reshape(-1, rows).contiguous()
@@ -141,16 +144,134 @@ def sharded_group_compute(group, x: torch.Tensor):
             v.copy_(m._local_matmul(x, m).reshape(-1))
     else:
         gemv_4bit_grouped(x, [(m.packed, m.state, m.bias, m.block_base, v) for m, v in zip(ms, views)])
+    lead = x.shape[:-1]
+    if not ms[0].gather:  # column-parallel: each member keeps its shard
+        return [v.view(*lead, r) for v, r in zip(views, rows)]
     P = ms[0].world_size
     gathered = torch.empty(P * S, dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(gathered, buf, group=ms[0].group)
     g2 = gathered.view(P, S)
-    lead = x.shape[:-1]
     outs, o = [], 0
     for r in rows:
         outs.append(g2[:, o:o + r].reshape(*lead, P * r))
         o += r
     return outs
+
+
+def consumer_absmax(qs: QuantState) -> torch.Tensor:
+    """Per-block fp32 absmax exactly as the kernels rebuild it (core.py:467-468:
+    code2[q] * absmax2[b / bs2], then + offset, two fp32 roundings)."""
+    if not qs.nested:
+        return qs.absmax
+    nb = qs.absmax.numel()
+    idx = torch.arange(nb, device=qs.absmax.device) // qs.state2.blocksize
+    prod = qs.state2.code[qs.absmax.long()].float() * qs.state2.absmax[idx].float()
+    return prod + qs.offset.float()
+
+
+@dataclass
+class ColShard:
+    """One rank's input columns [k0, k1) of every row of a 4-bit weight."""
+    packed: torch.Tensor          # u8, re-packed [M, (k1-k0)/2] row-major
+    state: QuantState             # shape (M, k1-k0), fp32 per-block absmax (double quant resolved)
+    k0: int
+    k1: int
+
+
+def shard_cols(packed: torch.Tensor, qs: QuantState, rank: int, world: int) -> ColShard:
+    """Slice input columns [rank*K/world, (rank+1)*K/world) of every row (row-parallel
+    layers).  Blocks stay whole (K/world must be a multiple of blocksize); the
+    rows' bytes are re-packed contiguously and the per-block scales become the
+    fp32 values the kernel would have rebuilt, so every local product is
+    bit-identical to the full layer's."""
+    M, K = int(qs.shape[0]), int(qs.shape[1])
+    if K % world != 0:
+        raise ValueError(f"in_features {K} is not divisible by world size {world}")
+    Kp = K // world
+    bs = qs.blocksize
+    if Kp % bs != 0 or K % bs != 0:
+        raise ValueError(f"column shard width {Kp} must be a multiple of blocksize {bs}")
+    k0, k1 = rank * Kp, (rank + 1) * Kp
+    loc = packed.reshape(M, K // 2)[:, k0 // 2:k1 // 2].contiguous().reshape(-1, 1)
+    am = consumer_absmax(qs).reshape(M, K // bs)[:, k0 // bs:k1 // bs].contiguous().reshape(-1)
+    st = QuantState(absmax=am, shape=torch.Size([M, Kp]), code=qs.code, blocksize=bs, quant_type=qs.quant_type,
+                    dtype=qs.dtype)
+    return ColShard(loc, st, k0, k1)
+
+
+class RowParallelLinear4bit(nn.Module):
+    """Megatron row-parallel 4-bit layer: this rank's input columns; takes the
+    LOCAL slice of the activation (the output of a column-parallel layer) and
+    all-reduces the partial products.  The bias is added once (rank 0)."""
+
+    def __init__(self, full: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
+                 group=None, local_matmul: Optional[Callable] = None):
+        super().__init__()
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world_size = dist.get_world_size(group) if world_size is None else world_size
+        self.group = group
+        sh = shard_cols(full.weight.data, full.weight.quant_state, self.rank, self.world_size)
+        self.register_buffer("packed", sh.packed, persistent=False)
+        self.state = sh.state
+        self.block_base = 0
+        self.k0, self.k1 = sh.k0, sh.k1
+        self.in_features = full.in_features
+        self.out_features = full.out_features
+        bias = None if (full.bias is None or self.rank != 0) else full.bias.data.clone()
+        self.register_buffer("bias", bias, persistent=False)
+        self._local_matmul = local_matmul  # test hook; None = the fused HIP kernels
+
+    def forward(self, x_local: torch.Tensor) -> torch.Tensor:
+        if x_local.shape[-1] != self.k1 - self.k0:
+            raise ValueError(f"row-parallel layer expects its {self.k1 - self.k0}-wide input slice, "
+                             f"got {x_local.shape[-1]}")
+        if self._local_matmul is not None:
+            y = self._local_matmul(x_local, self)
+        else:
+            from .core import gemm_4bit, gemv_4bit
+            if x_local.numel() == x_local.shape[-1]:
+                y = gemv_4bit(x_local, self.packed, state=self.state, bias=self.bias)
+            else:
+                y = gemm_4bit(x_local, self.packed, self.state, bias=self.bias)
+        y = y.contiguous()
+        dist.all_reduce(y, group=self.group)
+        return y
+
+
+# (column-parallel, row-parallel) projection names per block kind
+TP_BLOCKS = ((("q_proj", "k_proj", "v_proj"), "o_proj"), (("gate_proj", "up_proj"), "down_proj"))
+
+
+def apply_tensor_parallel(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
+                          group=None, local_matmul: Optional[Callable] = None) -> int:
+    """Megatron-style TP pairing over the Linear4bit layers of a decoder
+    (SURVEY.md 8f row 3): q/k/v and gate/up become column-parallel (each rank
+    keeps its attention heads / MLP columns, no collective), o_proj and
+    down_proj row-parallel (one all-reduce each) -- two collectives per layer
+    instead of one per Linear.  Attention then runs on the rank's local heads
+    (transformers infers the head count from the projection width and sizes the
+    KV cache lazily).  Returns the number of blocks converted."""
+    from .modules import Linear4bit
+
+    rank = dist.get_rank(group) if rank is None else rank
+    world = dist.get_world_size(group) if world_size is None else world_size
+    n = 0
+    for parent in list(model.modules()):
+        for cols, row in TP_BLOCKS:
+            mods = [parent._modules.get(nm) for nm in cols + (row,)]
+            if any(not isinstance(m, Linear4bit) for m in mods):
+                continue
+            if hasattr(parent, "head_dim") and cols[0] == "q_proj":
+                hd = parent.head_dim
+                for m in mods[:3]:
+                    if (m.out_features // hd) % world != 0:
+                        raise ValueError(f"{m.out_features // hd} heads do not split over {world} ranks")
+            for nm in cols:
+                parent._modules[nm] = RowShardedLinear4bit(parent._modules[nm], rank, world, group, local_matmul,
+                                                           gather=False)
+            parent._modules[row] = RowParallelLinear4bit(parent._modules[row], rank, world, group, local_matmul)
+            n += 1
+    return n
 
 
 def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,

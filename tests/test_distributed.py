@@ -171,3 +171,103 @@ def test_row_sharded_projection_group_single_gather():
         assert p.exitcode == 0
     for rank, ok in res:
         assert ok, f"rank {rank}: grouped sharded outputs differ from the full layers"
+
+
+def _tp_hook(x, mod):
+    """Test hook: a shard's local product from its own packed bytes + statistics
+    (oracle dequant; double quant resolved exactly as the kernels do)."""
+    import oracle
+    from quantizations_amd.parallel import consumer_absmax
+
+    st = mod.state
+    M, K = int(st.shape[0]), int(st.shape[1])
+    nb = M * K // st.blocksize
+    am = consumer_absmax(st)[mod.block_base:mod.block_base + nb]
+    W = torch.from_numpy(oracle.dequantize_4bit(mod.packed.numpy(), am.numpy(), M * K, st.blocksize,
+                                                st.quant_type)).reshape(M, K)
+    y = x.float() @ W.t()
+    if mod.bias is not None:
+        y = y + mod.bias.float()
+    return y.to(x.dtype)
+
+
+def _tp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import copy
+
+        import oracle
+        from transformers import LlamaConfig, LlamaForCausalLM
+
+        from quantizations_amd.core import Params4bit
+        from quantizations_amd.integration import fuse_projection_groups
+        from quantizations_amd.modules import Linear4bit
+        from quantizations_amd.parallel import RowParallelLinear4bit, apply_tensor_parallel
+
+        cfg = LlamaConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
+                          num_key_value_heads=2, vocab_size=97)
+        torch.manual_seed(0)
+        model = LlamaForCausalLM(cfg).float().eval()
+        ref = copy.deepcopy(model)
+        seed = 0
+        for name, lin in list(model.named_modules()):
+            if not isinstance(lin, torch.nn.Linear) or name == "lm_head":
+                continue
+            seed += 1
+            M, K = lin.out_features, lin.in_features
+            qt = "nf4" if ".layers.0." in name else "fp4"   # one format per layer: groups need it
+            W = lin.weight.detach().half()
+            st = oracle.quantize_4bit(W.float().numpy(), 64, qt, double_quant=True)
+            from quantizations_amd.core import QuantState, create_dynamic_map, get_4bit_type
+            qs = QuantState(absmax=torch.from_numpy(st.qabsmax), shape=torch.Size([M, K]),
+                            code=get_4bit_type(qt, "cpu"), blocksize=64, quant_type=qt, dtype=torch.float16,
+                            offset=torch.tensor(float(st.offset)),
+                            state2=QuantState(absmax=torch.from_numpy(st.absmax2), blocksize=256,
+                                              code=create_dynamic_map(), dtype=torch.float32))
+            l4 = Linear4bit(K, M, bias=False, quant_type=qt, device="meta")
+            l4.weight = Params4bit.from_prequantized(torch.from_numpy(st.packed).reshape(-1, 1),
+                                                     qs.as_dict(packed=True), device="cpu", module=l4)
+            parent = model.get_submodule(name.rsplit(".", 1)[0])
+            parent._modules[name.rsplit(".", 1)[1]] = l4
+            ref.get_submodule(name).weight.data.copy_(torch.from_numpy(oracle.dequantize(st)).reshape(M, K))
+        n = apply_tensor_parallel(model, rank, world, local_matmul=_tp_hook)
+        groups = fuse_projection_groups(model)
+        ids = torch.tensor([[5, 17, 3, 88, 41, 9]])
+        with torch.no_grad():
+            ref_logits = ref(input_ids=ids).logits
+            out = model(input_ids=ids, use_cache=True)
+            # one decode step through the (column-parallel) groups and the local-head KV cache
+            nxt = out.logits[:, -1:].argmax(-1)
+            step = model(input_ids=nxt, past_key_values=out.past_key_values, use_cache=True).logits
+            ref_step = ref(input_ids=torch.cat([ids, nxt], 1)).logits[:, -1:]
+        rel = float((out.logits - ref_logits).norm() / ref_logits.norm())
+        rel_step = float((step - ref_step).norm() / ref_step.norm())
+        o_proj = model.model.layers[0].self_attn.o_proj
+        q.put((rank, n, groups, rel, rel_step, isinstance(o_proj, RowParallelLinear4bit),
+               model.model.layers[0].self_attn.q_proj.packed.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tensor_parallel_pairing_tiny_llama():
+    """Megatron TP pairing (column q/k/v/gate/up, row o/down + all-reduce) on a
+    tiny Llama over gloo world 2: logits of prefill and of a cached decode step
+    equal the unsharded model's (fp32 sums in another order)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
+        os.environ.get("PYTHONPATH", "")
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, n, groups, rel, rel_step, is_rowpar, qshape in res:
+        assert n == 4 and groups == 4 and is_rowpar, (rank, n, groups)
+        assert qshape == 128 * 64 // 2   # q_proj rows 64 of 128 on each rank
+        assert rel < 1e-5 and rel_step < 1e-5, (rank, rel, rel_step)

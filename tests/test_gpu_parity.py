@@ -644,3 +644,43 @@ def test_fused_groups_hip_graph_capture():
         ref = torch.nn.functional.linear(x.float(), m.dequantize().float())
         rel = (o.float() - ref).norm() / ref.norm()
         assert rel < 2e-3, (name, rel)
+
+
+def test_tensor_parallel_pair_world1_rccl():
+    """apply_tensor_parallel through the real kernels and RCCL (world size 1):
+    column-parallel q/k/v/gate/up, row-parallel o/down (re-packed column slice,
+    fp32 per-block absmax resolved from the double quant) + all-reduce; logits
+    equal the unsharded quantised model's."""
+    import socket
+
+    import torch.distributed as dist
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import fuse_projection_groups, replace_with_bnb_linear
+    from quantizations_amd.parallel import RowParallelLinear4bit, apply_tensor_parallel
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                          num_key_value_heads=2, vocab_size=512)
+        torch.manual_seed(3)
+        model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+        replace_with_bnb_linear(model, quant_type="nf4")
+        ids = torch.randint(0, 512, (1, 7), device=DEV)
+        with torch.no_grad():
+            ref = model(input_ids=ids).logits.float()
+            assert apply_tensor_parallel(model, 0, 1) == 2 * cfg.num_hidden_layers
+            assert isinstance(model.model.layers[1].mlp.down_proj, RowParallelLinear4bit)
+            fuse_projection_groups(model)
+            out = model(input_ids=ids, use_cache=True)
+            nxt = out.logits[:, -1:].argmax(-1)
+            step = model(input_ids=nxt, past_key_values=out.past_key_values, use_cache=True).logits.float()
+        assert ((out.logits.float() - ref).norm() / ref.norm()) < 2e-3
+        assert torch.isfinite(step).all()
+    finally:
+        dist.destroy_process_group()

@@ -209,7 +209,22 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(b2b)
     b2b_us = e0.elapsed_time(e1) * 1e3 / iters
-    return statistics.mean(us), statistics.median(us), b2b_us
+    # one-shot read floor of the same 8.39 MB packed weight (same rotation, same timing method)
+    sink = torch.zeros(1, dtype=torch.int32, device=dev)
+    floor_fn = _lib.lib.qz_bench_read_floor
+
+    def floor():
+        e0.record()
+        for i in range(iters):
+            p = sets[i % copies][0]
+            rc = floor_fn(p.data_ptr(), p.numel(), sink.data_ptr(), stream)
+            if rc:
+                raise RuntimeError(f"qz_bench_read_floor rc={rc}")
+        e1.record()
+
+    blocked(floor)
+    floor_us = e0.elapsed_time(e1) * 1e3 / iters
+    return statistics.mean(us), statistics.median(us), b2b_us, floor_us
 
 
 @torch.inference_mode()
@@ -351,8 +366,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     if args.gemv_only:
-        mean_us, med_us, b2b_us = gemv_roofline()
+        mean_us, med_us, b2b_us, floor_us = gemv_roofline()
         print(json.dumps({"gemv_4096_us_mean": mean_us, "gemv_4096_us_median": med_us, "back_to_back_us": b2b_us,
+                          "read_floor_us": floor_us,
                           "achieved_GBs": GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9}), flush=True)
         return
 
@@ -402,7 +418,7 @@ def main():
     if rank == 0 and not args.no_roofline:
         del model
         torch.cuda.empty_cache()
-        mean_us, med_us, b2b_us = gemv_roofline()
+        mean_us, med_us, b2b_us, floor_us = gemv_roofline()
         # average launch duration = HIP events around `iters` back-to-back launches on
         # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
         # overhead on ROCm and disagrees with rocprofv3, so it is reported only.
@@ -416,7 +432,9 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_gemv_4bit<LUT16,DQ,f16,R=2,WK=1> 4096x4096 NF4+DQ",
                 "launch_us_avg": round(b2b_us, 3),
-                "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3)}
+                "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
+                "one_shot_read_floor_us": round(floor_us, 3),
+                "frac_of_one_shot_floor": round(floor_us / b2b_us, 4)}
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:

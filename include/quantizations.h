@@ -177,6 +177,11 @@ int qz_dequantize_4bit(const unsigned char *A, long long n, int quant_type, int 
                        const unsigned char *qabsmax, const float *absmax2, const float *code2, const float *offset,
                        int blocksize2, void *out, int out_dtype, void *stream);
 
+/* Measurement helper (bench.py's roofline context, not on the product path):
+ * one non-temporal 16-B read per thread over `bytes` of device memory -- the
+ * one-shot HBM read floor of a buffer the GEMV's size. */
+int qz_bench_read_floor(const void *p, long long bytes, unsigned int *sink, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

@@ -1,0 +1,31 @@
+// bench_floor.hip -- measurement helper (not on the product path): the
+// one-shot HBM read floor for a buffer of the GEMV's size.  Every thread
+// streams 16 B with a non-temporal load, exactly the GEMV's access width, and
+// the workgroup count is the buffer / 4 KiB; nothing is written unless a
+// sentinel matches, so the kernel time is launch + ramp + one pass of reads.
+// bench.py reports it beside the GEMV so roofline.frac can be read against what
+// a single launch can reach on the box.
+#include "common.h"
+
+namespace qz {
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_read_floor(const unsigned char *__restrict__ p, long long bytes,
+                                                    uint32_t *sink) {
+  const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+  uint32_t acc = 0;
+  if (c < bytes / 16) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p) + c);
+    acc = v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+}  // namespace qz
+
+extern "C" int qz_bench_read_floor(const void *p, long long bytes, unsigned int *sink, void *stream) {
+  if (!p || !sink || bytes < 16) return QZ_ERR_ARG;
+  const long long chunks = bytes / 16;
+  hipLaunchKernelGGL(qz::k_read_floor, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const unsigned char *>(p), bytes, sink);
+  QZ_LAUNCH_CHECK();
+  return QZ_OK;
+}

@@ -43,6 +43,10 @@ sys.path.insert(0, REPO)
 LLAMA3_8B = dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
                  num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
                  rms_norm_eps=1e-5, tie_word_embeddings=False)
+LLAMA3_70B = dict(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                  num_key_value_heads=8, vocab_size=128256, rope_theta=500000.0, max_position_embeddings=8192,
+                  rms_norm_eps=1e-5, tie_word_embeddings=False)
+MODELS = {"llama3-8b": LLAMA3_8B, "llama3-70b": LLAMA3_70B}
 # Linear4bit shapes of one Llama-3-8B layer (q, k, v, o, gate, up, down) as (M, K)
 LAYER_SHAPES = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
 GEMV_BYTES_4096 = 8_672_324  # packed 8,388,608 + qabsmax 262,144 + absmax2 4,096 + offset 4 + code2 1,024 + LUT 64
@@ -54,12 +58,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_model(layers: int, seed: int):
+def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_type: str = "nf4",
+                double_quant: bool = True):
     from transformers import LlamaConfig, LlamaForCausalLM
 
     from quantizations_amd.integration import replace_with_bnb_linear
 
-    cfg = LlamaConfig(**{**LLAMA3_8B, "num_hidden_layers": layers})
+    base = MODELS[model_name]
+    cfg = LlamaConfig(**{**base, "num_hidden_layers": layers or base["num_hidden_layers"]})
     torch.manual_seed(seed)
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.float16)
@@ -67,7 +73,8 @@ def build_model(layers: int, seed: int):
         model = LlamaForCausalLM(cfg)
     torch.set_default_dtype(prev)
     model.eval()
-    replace_with_bnb_linear(model, modules_to_not_convert=["lm_head"], quant_type="nf4", compress_statistics=True,
+    replace_with_bnb_linear(model, modules_to_not_convert=["lm_head"], quant_type=quant_type,
+                            compress_statistics=double_quant,
                             compute_dtype=torch.float32)
     torch.cuda.empty_cache()
     return model, cfg
@@ -339,7 +346,11 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--prompt", type=int, default=32)
-    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--layers", type=int, default=0, help="decoder layers (0 = the model's own count)")
+    ap.add_argument("--model", choices=sorted(MODELS), default="llama3-8b",
+                    help="llama3-8b (configs #1-#4) or llama3-70b (config #5)")
+    ap.add_argument("--quant", choices=("nf4", "fp4"), default="nf4", help="codebook (config #3: fp4 --no-dq)")
+    ap.add_argument("--no-dq", action="store_true", help="fp32 absmax instead of double quant")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the decode step")
     ap.add_argument("--no-roofline", action="store_true")
@@ -380,7 +391,8 @@ def main():
         return
 
     t_build = time.perf_counter()
-    model, cfg = build_model(args.layers, seed=0)
+    model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
+                             double_quant=not args.no_dq)
     if sharded:
         if args.tp_mode == "pair":
             from quantizations_amd.parallel import apply_tensor_parallel
@@ -451,7 +463,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
-            "config": {"workload": "llama3-8b-nf4-dq-decode-bs1", "layers": args.layers,
+            "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}-decode-bs1",
+                       "layers": cfg.num_hidden_layers,
                        "prompt_len": args.prompt, "batch": 1, "decode": mode,
                        "parallelism": ("single" if not sharded else
                                        f"tp{world}-megatron-pair-allreduce" if args.tp_mode == "pair" else

@@ -181,6 +181,14 @@ int main(int argc, char **argv) {
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, XL, ABL>), dim3(g), dim3(NW * 64), XL ? K * 2 : 0, 0, q); })
   const bool ablate = argc > 4 && std::string(argv[4]) == "ablate";
+  const bool small = argc > 4 && std::string(argv[4]) == "small";
+  if (small) {  // geometry around the 4096^2 headline launch (workgroup size too)
+    GVN(1, true, 2, 1, 4); GVN(1, true, 1, 1, 4); GVN(1, true, 1, 2, 4); GVN(1, true, 2, 2, 4);
+    GVN(1, true, 2, 1, 8); GVN(1, true, 1, 1, 8); GVN(1, true, 1, 2, 8); GVN(1, true, 2, 2, 8);
+    GVN(1, true, 2, 1, 16); GVN(1, true, 1, 1, 16); GVN(1, true, 1, 2, 16); GVN(1, true, 2, 2, 16);
+    GVN(2, true, 2, 1, 4); GVN(2, true, 1, 1, 16);
+    GVF(2, true, 2, 1, 4, false, 3); GVF(2, true, 2, 1, 4, false, 7);
+  }
   if (ablate) {
     GV(1, true, 4, 2); GV(1, true, 2, 1); GV(0, true, 4, 2); GV(2, true, 4, 2);
     GVF(1, true, 4, 2, 4, false, 1); GVF(1, true, 4, 2, 4, false, 2); GVF(1, true, 4, 2, 4, false, 3);
@@ -188,7 +196,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate) {
+  if (!ablate && !small) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

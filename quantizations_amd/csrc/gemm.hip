@@ -32,6 +32,7 @@
 // Requires K % 64 == 0, blocksize >= 64 (every Llama shape); other shapes
 // return QZ_ERR_SHAPE and the host falls back to dequantize + library GEMM.
 #include "common.h"
+#include "decode.h"
 
 namespace qz {
 
@@ -41,70 +42,6 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kBM = 128, kBK = 64;
-
-__device__ __forceinline__ uint32_t gperm(uint32_t s0, uint32_t s1, uint32_t sel) {
-  return __builtin_amdgcn_perm(s0, s1, sel);
-}
-
-// fp32 pair -> packed 16-bit pair, round-to-nearest-even (bit-exact with the
-// dequant kernel's stores; see common.h on the scalar-convert tie bug)
-template <int DT> __device__ __forceinline__ uint32_t cvt_pk16(float lo, float hi) {
-  if constexpr (DT == QZ_DT_F16) {
-    return cvt_pk_f16_rne(lo, hi);
-  } else {
-    uint32_t r;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-    return r;
-  }
-}
-
-// fp32 FP4 dequant-tree magnitudes (kernels.cu:70-111; sign = bit 3); NF4 uses
-// kNF4 (kernels.cu:851) from common.h
-__device__ __constant__ static const float kFP4Mag[8] = {0.00000000f, 5.208333333e-03f, 0.66666667f, 1.00000000f,
-                                                         0.33333333f, 0.50000000f,      0.16666667f, 0.25000000f};
-
-// 16-entry table of one (row, block): entries fp16/bf16(code[i] * am) as byte
-// planes t[0..3] = low bytes of entries 0-3, 4-7, 8-11, 12-15 and t[4..7] =
-// high bytes (the layout decode_codes expects).
-template <int QT, int DT>
-__device__ __forceinline__ void block_table(float am, uint32_t (&t)[8]) {
-  uint32_t p[8];  // p[k] = (entry 2k, entry 2k+1)
-  if constexpr (QT == QZ_NF4) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p[k] = cvt_pk16<DT>(__fmul_rn(kNF4[2 * k], am), __fmul_rn(kNF4[2 * k + 1], am));
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      p[k] = cvt_pk16<DT>(__fmul_rn(kFP4Mag[2 * k], am), __fmul_rn(kFP4Mag[2 * k + 1], am));
-      p[4 + k] = p[k] ^ 0x80008000u;  // (c * am) * -1: exact sign flip, code 8 -> -0.0
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    t[j] = gperm(p[2 * j + 1], p[2 * j], 0x06040200u);
-    t[4 + j] = gperm(p[2 * j + 1], p[2 * j], 0x07050301u);
-  }
-}
-
-// 8 nibbles (one dword, high nibble = even element) -> 4 packed 16-bit pairs in
-// the order (e0,e2),(e4,e6),(e1,e3),(e5,e7): AND-combined 8-entry v_perm
-// lookups (see decode_lut16 in gemv.hip).
-__device__ __forceinline__ void decode_codes(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
-  uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);
-  asm("" : "+v"(ah));
-  const uint32_t bh = ah ^ 0x88888888u;
-  const uint32_t lh = gperm(t[1], t[0], ah) & gperm(t[3], t[2], bh);
-  const uint32_t hh = gperm(t[5], t[4], ah) & gperm(t[7], t[6], bh);
-  uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);
-  asm("" : "+v"(al));
-  const uint32_t bl = al ^ 0x88888888u;
-  const uint32_t ll = gperm(t[1], t[0], al) & gperm(t[3], t[2], bl);
-  const uint32_t hl = gperm(t[5], t[4], al) & gperm(t[7], t[6], bl);
-  P[0] = gperm(hh, lh, 0x05010400u);
-  P[1] = gperm(hh, lh, 0x07030602u);
-  P[2] = gperm(hl, ll, 0x05010400u);
-  P[3] = gperm(hl, ll, 0x07030602u);
-}
 
 // natural 8-element chunk (x0..x7 as 4 pairs) -> (x0,x2),(x4,x6),(x1,x3),(x5,x7)
 __device__ __forceinline__ v4u pair_order(const v4u r) {

@@ -299,6 +299,78 @@ def test_gemv_row_shard_block_base(orc):
             assert torch.equal(y, full[:, sh.r0:sh.r1]), (world, r)
 
 
+@pytest.mark.parametrize("bs", [128, 256, 1024, 4096])
+@pytest.mark.parametrize("qt,dq", [("nf4", True), ("fp4", False)])
+def test_gemv_grouped_gemm_dequant_other_blocksizes(orc, bs, qt, dq):
+    """blocksize != 64 through every consumer: GEMV, grouped GEMV (vs the oracle),
+    GEMM (vs fp64 of the dequantised weight) and the dequant kernel (bit-exact)."""
+    from quantizations_amd.core import dequantize_4bit, gemm_4bit, gemv_4bit, gemv_4bit_grouped, quantize_4bit
+
+    M, K = 256, 4096
+    W = _w(M, K, seed=bs)
+    x = _x(K, seed=bs + 1).to(DEV).reshape(1, K)
+    packed, st = quantize_4bit(W.to(DEV), blocksize=bs, quant_type=qt, compress_statistics=dq)
+    o = orc.quantize_4bit(W.float().numpy(), bs, qt, double_quant=dq)
+    yref = orc.gemv(x.float().cpu().numpy().ravel(), o)
+    assert_close(gemv_4bit(x, packed, state=st).float().cpu(), yref, torch.float16, f"gemv bs={bs}")
+    (yg,) = gemv_4bit_grouped(x, [(packed, st, None)])
+    assert_close(yg.float().cpu(), yref, torch.float16, f"grouped bs={bs}")
+    wd = dequantize_4bit(packed, st).t()
+    ow = orc.dequantize(o).astype(np.float16).reshape(M, K)
+    assert np.array_equal(wd.cpu().numpy().view(np.int16), ow.view(np.int16)), f"dequant bs={bs}"
+    X = torch.randn(40, K, generator=torch.Generator().manual_seed(bs)).half().to(DEV)
+    Y = gemm_4bit(X, packed, st, route="fused")
+    assert_close(Y.float().cpu(), (X.double() @ wd.double().t()).cpu().numpy(), torch.float16, f"gemm bs={bs}")
+
+
+@pytest.mark.parametrize("M,K", [(8192, 28672), (28672, 8192), (10240, 8192)])
+def test_gemv_llama70b_shapes_vs_fp64_of_dequant(M, K):
+    """Full Llama-3-70B shapes (down, gate/up, fused q/k/v): GEMV vs an fp64 product
+    of the bit-exact dequantised weight (the oracle is too slow at 235 M weights; the
+    dequant kernel is pinned to it bit for bit at smaller sizes)."""
+    from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
+
+    torch.manual_seed(M + K)
+    W = (torch.randn(M, K, device=DEV) * 0.02).half()
+    packed, st = quantize_4bit(W, quant_type="nf4")
+    del W
+    x = torch.randn(1, K, device=DEV).half()
+    y = gemv_4bit(x, packed, state=st)
+    wd = dequantize_4bit(packed, st, out_dtype=torch.float32).t()   # [M, K] fp32 = the reference's weight products
+    ref = (wd.double() @ x.double().reshape(K, 1)).reshape(1, M)
+    del wd
+    assert_close(y.float().cpu(), ref.cpu().numpy(), torch.float16, f"gemv {M}x{K}")
+
+
+@pytest.mark.parametrize("act", [torch.bfloat16, torch.float32])
+def test_linear4bit_bf16_fp32_activations_and_compute_dtype(orc, act):
+    """Linear4bit with bf16/fp32 inputs (compute_dtype follows the input, reference
+    modules.py:112-122): decode and prefill outputs keep the input dtype.  Decode is
+    checked against the fp16 dequantised weight (the GEMV keeps fp16 codes x fp32
+    scales); prefill against the weight in the activation dtype that the kernels
+    multiply: dequantize_4bit(out_dtype=act), i.e. bf16(code*absmax) rounded once.
+    (The reference's bf16 path multiplies W.to(bf16) of the fp16 dequant, modules.py:64,
+    a double rounding that differs by one bf16 ulp on ~1/16 of the weights -- the
+    output difference that makes is ~2^-9 relative)"""
+    import quantizations_amd as qa
+
+    torch.manual_seed(5)
+    lin = torch.nn.Linear(1024, 768, bias=True)
+    m = qa.Linear4bit(1024, 768, bias=True, quant_type="nf4")
+    m.weight = qa.Params4bit(lin.weight.data.half(), requires_grad=False, quant_type="nf4", module=m)
+    m.bias = torch.nn.Parameter(lin.bias.data.clone(), requires_grad=False)
+    m = m.to(DEV)
+    Wd = m.dequantize().double()
+    for shape in ((1, 1, 1024), (3, 5, 1024)):
+        x = torch.randn(*shape, generator=torch.Generator().manual_seed(sum(shape))).to(act)
+        y = m(x.to(DEV))
+        assert y.dtype == act and y.shape == (*shape[:-1], 768)
+        Wop = Wd if shape[1] == 1 else \
+            qa.dequantize_4bit(m.weight, m.weight.quant_state, out_dtype=act if act != torch.float32 else None).t().double()
+        ref = x.double().reshape(-1, 1024) @ Wop.t().cpu() + lin.bias.detach().double()
+        assert_close(y.float().cpu().reshape(-1, 768), ref.numpy(), act, f"{act} {shape}")
+
+
 GROUPED_SETS = [  # (segment rows, K): Llama-3-8B q/k/v and gate/up, plus odd and tiny cases
     ((4096, 1024, 1024), 4096), ((14336, 14336), 4096), ((512, 128, 128), 1024), ((37, 5, 64, 3), 2112),
     ((7, 9), 96), ((3, 4), 62)]

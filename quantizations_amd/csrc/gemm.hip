@@ -212,6 +212,115 @@ __global__ __launch_bounds__(256) void k_gemm_4bit(GemmParams p) {
   }
 }
 
+// Multi-token GEMV for 2 <= T <= 16 (small-batch decode, short prefills).
+// A 512-thread workgroup owns 16 weight rows; its 8 waves split K and meet in
+// LDS (no workspace, no second launch).  Per 256-element chunk, lane
+// (r = l % 16, g = l / 16) of a wave loads the 32 B of row r holding codes
+// 64g .. 64g+63 -- one whole scale block, and with its 3 neighbours a full
+// 128-B line of the row -- builds that block's exact 16-bit table and decodes
+// its 8 dwords into the A fragments of 8 v_mfma_f32_16x16x32 (A = weights, M
+// dimension; B = the T tokens, N dimension, zero-padded to 16, loaded by lane
+// (c = l % 16, g) from L2 in the same pair order).  Every token rides on the
+// same decode: T tokens cost about one GEMV.
+constexpr int kMtChunk = 256, kMtWaves = 8;
+template <int QT, bool DQ, int DT>
+__global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
+  __shared__ float s_code2[DQ ? 256 : 1];
+  __shared__ f4_t s_red[kMtWaves][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 16;
+  const int nch = p.K / kMtChunk;
+  const int ch0 = wave * nch / kMtWaves, ch1 = (wave + 1) * nch / kMtWaves;
+  const int wrow = min(m0 + r, p.M - 1);
+  const uint32_t row_bytes = (uint32_t)p.K >> 1;
+  const unsigned char *wptr = p.B + (size_t)wrow * row_bytes + 32 * g;
+  const long long ebase = (long long)wrow * p.K + 64 * g;
+  const bool tok = r < p.T;  // as a B-operand lane, lane l carries token c = l % 16
+  const uint16_t *xrow = reinterpret_cast<const uint16_t *>(p.X) + (size_t)min(r, p.T - 1) * p.ldx + 64 * g;
+
+  // two NAMED stages (a dynamically indexed register array would live in scratch)
+  // (the token fragments are loaded at consume time: each B-fragment load touches
+  // 64 lines, and keeping two sets in flight measured slower at T = 16)
+  struct Stage {
+    v4u w[2];
+    uint32_t q;
+    float a;
+    int ch;
+  };
+  auto load = [&](Stage &st, int ch) {
+    const v4u *wp = reinterpret_cast<const v4u *>(wptr + ch * (kMtChunk / 2));
+    st.w[0] = __builtin_nontemporal_load(wp);
+    st.w[1] = __builtin_nontemporal_load(wp + 1);
+    st.ch = ch;
+    const uint32_t b = (uint32_t)((ebase + ch * kMtChunk) >> p.bs_log2);
+    if constexpr (DQ) {
+      st.q = p.sc.qabsmax[b];
+      st.a = p.sc.absmax2[b >> p.bs2_log2];
+    } else {
+      st.q = 0u;
+      st.a = p.sc.absmax[b];
+    }
+  };
+  f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
+  float offset = 0.0f;
+  auto consume = [&](const Stage &st) {
+    v4u x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = *reinterpret_cast<const v4u *>(xrow + st.ch * kMtChunk + 8 * j);
+    float am;
+    if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[st.q], st.a), offset);
+    else am = st.a;
+    uint32_t t[8];
+    block_table<QT, DT>(am, t);
+    const uint32_t w[8] = {st.w[0].x, st.w[0].y, st.w[0].z, st.w[0].w, st.w[1].x, st.w[1].y, st.w[1].z, st.w[1].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t P[4];
+      decode_codes(w[j], t, P);
+      const v4u af = v4u{P[0], P[1], P[2], P[3]};
+      const v4u bf = tok ? pair_order(x[j]) : v4u{0u, 0u, 0u, 0u};
+      if constexpr (DT == QZ_DT_F16)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, af), __builtin_bit_cast(h8_t, bf), acc,
+                                                     0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, af), __builtin_bit_cast(b8_t, bf),
+                                                      acc, 0, 0, 0);
+    }
+  };
+  Stage s0, s1;
+  if (ch0 < ch1) load(s0, ch0);  // first HBM requests go out before anything else
+  if constexpr (DQ) {
+    if (tid < 256) s_code2[tid] = p.sc.code2[tid];
+    offset = *p.sc.offset;
+    __syncthreads();
+  }
+  for (int ch = ch0; ch < ch1; ch += 2) {  // ping-pong: the next stage is in flight during each decode
+    if (ch + 1 < ch1) load(s1, ch + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    consume(s0);
+    if (ch + 1 >= ch1) break;
+    if (ch + 2 < ch1) load(s0, ch + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    consume(s1);
+  }
+  // K-split partials meet in LDS; C/D map: lane l holds rows 4g+i (i = 0..3) for token l % 16
+  s_red[wave][lane] = acc;
+  __syncthreads();
+  if (tid < 256) {
+    const int l = tid & 63, i = tid >> 6;  // (lane slot, row-in-quad)
+    const int c = l & 15, m = m0 + 4 * (l >> 4) + i;
+    if (c < p.T && m < p.M) {
+      float v = 0.0f;
+#pragma unroll
+      for (int w = 0; w < kMtWaves; ++w) v += s_red[w][l][i];
+      if (p.bias) v += load_f32<DT>(p.bias, m);
+      store_f32<DT>(p.Y, (long long)c * p.ldy + m, v);
+    }
+  }
+}
+
 // Y[t, m] = sum_z ws[z][t][m] (+ bias[m]); 4 consecutive m per thread.
 template <int DT>
 __global__ __launch_bounds__(256) void k_gemm_reduce(const float *__restrict__ ws, int nsplit, int T, int M,
@@ -258,8 +367,11 @@ static void gemm_plan(int T, int M, int K, long long ws_bytes, int *bt, int *nsp
 
 using namespace qz;
 
+static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0; }
+
 extern "C" long long qz_gemm_4bit_workspace_size(int T, int M, int K) {
   if (T <= 0 || M <= 0 || K <= 0 || K % kBK != 0) return 0;
+  if (mt_ok(T, K)) return 0;  // the multi-token kernel reduces in LDS
   int bt, ns, ks;
   gemm_plan(T, M, K, (long long)1 << 62, &bt, &ns, &ks);
   return ns > 1 ? (long long)ns * T * M * 4 : 0;
@@ -298,10 +410,27 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
   p.bs_log2 = bsl;
   p.bs2_log2 = bs2l;
   int bt, nsplit;
+  hipStream_t s = (hipStream_t)stream;
+  if (mt_ok(T, K)) {  // 2..16 tokens: multi-token MFMA GEMV, one launch
+    p.ws = nullptr;
+    p.k_split = K;
+    const dim3 grid((unsigned)((M + 15) / 16));
+#define QZ_MT(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemv_4bit_mt<QT_, DQ_, DT_>), grid, dim3(64 * kMtWaves), 0, s, p)
+#define QZ_MT_DT(QT_, DQ_) \
+  do { if (dtype == QZ_DT_F16) QZ_MT(QT_, DQ_, QZ_DT_F16); else QZ_MT(QT_, DQ_, QZ_DT_BF16); } while (0)
+    if (quant_type == QZ_FP4) {
+      if (dq) QZ_MT_DT(QZ_FP4, true); else QZ_MT_DT(QZ_FP4, false);
+    } else {
+      if (dq) QZ_MT_DT(QZ_NF4, true); else QZ_MT_DT(QZ_NF4, false);
+    }
+#undef QZ_MT_DT
+#undef QZ_MT
+    QZ_LAUNCH_CHECK();
+    return QZ_OK;
+  }
   gemm_plan(T, M, K, workspace ? workspace_bytes : 0, &bt, &nsplit, &p.k_split);
   p.ws = nsplit > 1 ? workspace : nullptr;
   const dim3 grid((unsigned)((M + kBM - 1) / kBM), (unsigned)((T + bt - 1) / bt), (unsigned)nsplit);
-  hipStream_t s = (hipStream_t)stream;
 #define QZ_GEMM(QT_, DQ_, DT_, BT_) hipLaunchKernelGGL((k_gemm_4bit<QT_, DQ_, DT_, BT_>), grid, dim3(256), 0, s, p)
 #define QZ_GEMM_BT(QT_, DQ_, DT_) \
   do { if (bt == 64) QZ_GEMM(QT_, DQ_, DT_, 64); else QZ_GEMM(QT_, DQ_, DT_, 128); } while (0)

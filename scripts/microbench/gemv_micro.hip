@@ -182,6 +182,11 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, XL, ABL>), dim3(g), dim3(NW * 64), XL ? K * 2 : 0, 0, q); })
   const bool ablate = argc > 4 && std::string(argv[4]) == "ablate";
   const bool small = argc > 4 && std::string(argv[4]) == "small";
+  const bool r8 = argc > 4 && std::string(argv[4]) == "r8";
+  if (r8) {  // 8 rows per wave (half the x traffic per weight byte) vs the production geometries
+    GV(1, true, 4, 2); GV(1, true, 2, 1); GV(1, true, 8, 1); GV(1, true, 8, 2); GV(1, true, 8, 4);
+    GVN(1, true, 8, 1, 8); GVN(1, true, 8, 2, 8);
+  }
   if (small) {  // geometry around the 4096^2 headline launch (workgroup size too)
     GVN(1, true, 2, 1, 4); GVN(1, true, 1, 1, 4); GVN(1, true, 1, 2, 4); GVN(1, true, 2, 2, 4);
     GVN(1, true, 2, 1, 8); GVN(1, true, 1, 1, 8); GVN(1, true, 1, 2, 8); GVN(1, true, 2, 2, 8);
@@ -196,7 +201,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small) {
+  if (!ablate && !small && !r8) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

@@ -532,6 +532,49 @@ def test_gemm_random_activations_vs_fp64(dt, T, M, K):
     assert_close(Y.float().cpu(), ref.cpu().numpy(), dt, f"gemm vs fp64 {dt} {T}x{M}x{K}")
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("qt,dq", [("nf4", True), ("fp4", True), ("nf4", False)])
+@pytest.mark.parametrize("T,M,K", [(2, 4096, 4096), (3, 1028, 1280), (8, 14336, 4096), (16, 4096, 14336),
+                                   (16, 132, 256)])
+def test_multi_token_gemv_exact_operand_and_oracle(orc, qt, dq, dt, T, M, K):
+    """2..16 tokens take the multi-token MFMA GEMV: one-hot tokens read back
+    dequantize_4bit's weights bit for bit; random tokens match the oracle."""
+    from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
+
+    W = _w(M, K, seed=M + 3 * K + T)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+    ks = (torch.arange(T) * 389 + 7) % K
+    X1 = torch.zeros(T, K, dtype=dt)
+    X1[torch.arange(T), ks] = 1.0
+    Y1 = gemm_4bit(X1.to(DEV), packed, st, route="fused")
+    Wd = dequantize_4bit(packed, st, out_dtype=dt).t()
+    assert torch.equal(Y1, Wd[:, ks.to(DEV)].t()), f"one-hot {qt} dq={dq} {dt} {T}x{M}x{K}"
+    X = torch.randn(T, K, generator=torch.Generator().manual_seed(T * K)).to(dt)
+    bias = torch.randn(M, generator=torch.Generator().manual_seed(M)).to(dt)
+    Y = gemm_4bit(X.to(DEV), packed, st, bias=bias.to(DEV), route="fused")
+    ref = X.double() @ Wd.double().cpu().t() + bias.double()
+    assert_close(Y.float().cpu(), ref.numpy(), dt, f"mt {qt} dq={dq} {dt} {T}x{M}x{K}")
+
+
+def test_multi_token_gemv_without_workspace():
+    """Direct C-ABI call with no workspace: the multi-token kernel runs unsplit when
+    the K slice fits LDS, else the tiled kernel takes it -- same results."""
+    from quantizations_amd import _lib
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    for K in (1024, 4096):
+        T, M = 5, 512
+        W = _w(M, K, seed=K)
+        packed, st = quantize_4bit(W.to(DEV), quant_type="nf4")
+        X = torch.randn(T, K, generator=torch.Generator().manual_seed(1)).half().to(DEV)
+        Y = torch.empty(T, M, dtype=torch.float16, device=DEV)
+        _lib.check(_lib.lib.qz_gemm_4bit(T, M, K, X.data_ptr(), K, _lib.DT_F16, packed.data_ptr(), _lib.NF4, 64,
+                                         *st.scale_args(), 0, Y.data_ptr(), M, 0, 0,
+                                         torch.cuda.current_stream().cuda_stream), "gemm")
+        ref = gemm_4bit(X, packed, st, route="fused")
+        assert ((Y.double() - ref.double()).norm() / ref.double().norm()) < 1e-3
+
+
 def test_gemm_routes_agree_and_fallbacks():
     """route='fused' and route='dequant' multiply the same operand; shapes the
     fused kernel does not take (M % 4 != 0, fp32 input) fall back in 'auto'."""
@@ -559,8 +602,9 @@ def test_gemm_split_k_with_bias_matches_unsplit(orc):
     from quantizations_amd import _lib
     from quantizations_amd.core import gemm_4bit, quantize_4bit
 
-    T, M, K = 8, 1024, 8192
+    T, M, K = 20, 1024, 8192   # > 16 tokens: the tiled kernel, K split over workgroups
     assert _lib.lib.qz_gemm_4bit_workspace_size(T, M, K) > 0  # this shape does split
+    assert _lib.lib.qz_gemm_4bit_workspace_size(8, M, K) == 0  # 2..16 tokens reduce in LDS
     W = _w(M, K, seed=11)
     X = torch.randn(T, K, generator=torch.Generator().manual_seed(12)).half()
     bias = torch.randn(M, generator=torch.Generator().manual_seed(13)).half()

@@ -272,7 +272,11 @@ def prefill_bench(T: int = 16384, iters: int = 10):
             res[name] = {"ms": round(ms, 3), "TFLOP/s": round(2.0 * T * M * K / (ms * 1e-3) / 1e12, 1)}
         out[f"{M}x{K}"] = res
         del W, packed, qs
-    return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0}
+    from quantizations_amd.core import PREFILL_FUSED_MAX_TOKENS
+    return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0,
+            "product_route": "fused" if T <= PREFILL_FUSED_MAX_TOKENS else "dequant+hipblaslt",
+            "note": "both routes multiply the same bit-exact dequantised weight; matmul_4bit takes the fused "
+                    f"MFMA kernel up to {PREFILL_FUSED_MAX_TOKENS} tokens (profiles/r1_prefill_mfma_util.txt)"}
 
 
 @torch.inference_mode()

@@ -19,17 +19,19 @@
 // (1 KiB per wave instruction, fully coalesced) and non-temporal: each byte
 // is read exactly once per call.
 //
-// Nibble decode happens in VALU registers with v_perm_b32 byte lookups
-// (no LDS, no bank conflicts):
-//  * FP4 (sign/magnitude codebook): the 8 magnitudes x12 = {0,1/16,8,12,4,6,
-//    2,3} are exact in fp16 and all have a zero low byte, so one v_perm per 4
-//    nibbles yields the fp16 high bytes, the sign bit is OR-ed in, and one
-//    more v_perm per pair assembles half2 (e_2j, e_2j+1).  The x12 is undone
-//    once per output.  ~2 VALU ops per weight.
-//  * 16-entry codebooks (NF4, or any runtime codebook): fp16 low/high byte
-//    tables, two v_perm (entries 0-7 / 8-15) blended by v_bfi on bit 3,
-//    then pairs (e0,e2),(e4,e6),(e1,e3),(e5,e7) -- x is pre-permuted to match
-//    once per step.  ~3.5 VALU ops per weight.
+// Nibble decode (production: kModeTab).  A workgroup first writes a 256-entry
+// table to LDS: entry b = the two fp16 codes of packed byte b, i.e. exactly
+// the half2 operand that v_dot2 multiplies with the natural-order x pair.
+// Decoding a byte is then one address computation (2 VALU) and one
+// ds_read_b32; the table is stored 32 times, copy j wholly inside bank j, and
+// lane l reads copy l % 32, so the random byte values never conflict.  Any
+// 16-entry codebook works (NF4, FP4 x12 with the sign in bit 3, a runtime LUT).
+// The older register-only decodes are kept for the microbenchmarks:
+//  * kModeFP4: the 8 FP4 magnitudes x12 have zero low bytes, so one v_perm
+//    per 4 nibbles yields the fp16 high bytes and the sign bit is OR-ed in.
+//  * kModeLUT16: two 8-entry v_perm lookups per fp16 byte plane, AND-combined
+//    on bit 3, then pairs (e0,e2),(e4,e6),(e1,e3),(e5,e7).  ~3.5 VALU ops per
+//    weight, half of them half-rate v_perm: VALU-issue-bound on gfx950.
 // Products: v_dot2_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
 // per 32-element chunk the fp32 dot is scaled by the block absmax with one
 // FMA.  fp32/bf16 activations are split into hi+lo fp16 halves (x = xh + xl,
@@ -41,8 +43,20 @@ namespace qz {
 enum {
   kModeFP4 = 0,    // sign/magnitude FP4: 8-entry x12 table in VALU
   kModeLUT16 = 1,  // any 16-entry codebook (NF4): AND-combined v_perm lookups in VALU
-  kModeRaw = 2     // benchmark-only: no decode
+  kModeRaw = 2,    // benchmark-only: no decode
+  kModeTab = 3     // any 16-entry codebook: byte -> half2 table in LDS, bank-private copies
 };
+
+// kModeTab: one LDS entry per packed BYTE value holds the two decoded fp16
+// codes (element 2m in the low half, 2m+1 in the high half) -- exactly the
+// operand of v_dot2 against the natural-order x pair, so the decode is one
+// address computation + one ds_read_b32 per two weights and NO v_perm.  A
+// ds_read_b32 serves each 32-lane half of the wave in one LDS cycle when its
+// lanes hit distinct banks (MI355X_MICROARCH.md, LDS table); byte values are
+// random, so the table is stored 32 times, copy j entirely in bank j
+// (dword e*32 + j), and lane l reads copy l % 32: never a bank conflict.
+constexpr int kTabCopies = 32;
+constexpr int kTabDwords = 256 * kTabCopies;  // 32 KiB
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -176,7 +190,7 @@ template <int MODE, int DT> struct XSlice {
   // hi/lo half2 operands, pair order of MODE
   __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1]) const {
     if constexpr (DT == QZ_DT_F16) {
-      if constexpr (MODE == kModeFP4) {
+      if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) hi[i] = raw[i];
       } else {
@@ -203,7 +217,7 @@ template <int MODE, int DT> struct XSlice {
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         int a[4], b[4];
-        if constexpr (MODE == kModeFP4) {
+        if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
           a[0] = 0; b[0] = 1; a[1] = 2; b[1] = 3; a[2] = 4; b[2] = 5; a[3] = 6; b[3] = 7;
         } else {
           a[0] = 0; b[0] = 2; a[1] = 4; b[1] = 6; a[2] = 1; b[2] = 3; a[3] = 5; b[3] = 7;
@@ -249,6 +263,74 @@ __device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)
     }
   }
   return s0 + s1;
+}
+
+// kModeTab: dot of one lane's 16-byte chunk through the LDS byte table.
+// `jb` = 4 * (lane % 32) selects the lane's bank-private copy.
+// (ABL: benchmark-only ablations -- 16 replaces the dot products by integer
+// adds, 32 replaces the table reads by the addresses themselves.)
+template <bool SPLIT, int ABL = 0>
+__device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&hi)[16],
+                                               const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t *s_tab,
+                                               uint32_t jb) {
+  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  uint32_t v[16];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    // byte m of w, times 128 (the 32-dword stride of one entry), plus the copy
+    const uint32_t a0 = ((w[d] << 7) & 0x7F80u) | jb;
+    const uint32_t a1 = ((w[d] >> 1) & 0x7F80u) | jb;
+    const uint32_t a2 = ((w[d] >> 9) & 0x7F80u) | jb;
+    const uint32_t a3 = ((w[d] >> 17) & 0x7F80u) | jb;
+    if constexpr ((ABL & 32) != 0) {
+      v[4 * d + 0] = a0; v[4 * d + 1] = a1; v[4 * d + 2] = a2; v[4 * d + 3] = a3;
+    } else {
+      v[4 * d + 0] = *reinterpret_cast<const uint32_t *>(tb + a0);
+      v[4 * d + 1] = *reinterpret_cast<const uint32_t *>(tb + a1);
+      v[4 * d + 2] = *reinterpret_cast<const uint32_t *>(tb + a2);
+      v[4 * d + 3] = *reinterpret_cast<const uint32_t *>(tb + a3);
+    }
+  }
+  if constexpr ((ABL & 16) != 0) {
+    uint32_t u0 = 0, u1 = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i & 1) u1 += v[i] ^ hi[i];
+      else u0 += v[i] ^ hi[i];
+    }
+    return (float)(u0 + u1);
+  }
+  float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i & 1) s1 = dot2(v[i], hi[i], s1);
+    else s0 = dot2(v[i], hi[i], s0);
+    if constexpr (SPLIT) {
+      if (i & 1) s1 = dot2(v[i], lo[i], s1);
+      else s0 = dot2(v[i], lo[i], s0);
+    }
+  }
+  return s0 + s1;
+}
+
+// Builds the kModeTab byte table from the 16-entry fp16 byte planes t[8]
+// (every thread of the workgroup takes part; the caller synchronises).
+template <int NT>
+__device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t (&t)[8]) {
+  for (int e = threadIdx.x; e < 256; e += NT) {
+    uint32_t P[4];
+    decode_lut16((uint32_t)e, t, P);  // byte 0 = e: P[0].lo = code[e >> 4], P[2].lo = code[e & 15]
+    const uint32_t v = (P[0] & 0xFFFFu) | (P[2] << 16);
+    const u32x4 q = {v, v, v, v};
+    // 128 B per entry; rotate the 16-B pieces by lane so that each 8-lane
+    // store group covers all 32 banks
+#pragma unroll
+    for (int i = 0; i < kTabCopies / 4; ++i) {
+      const int piece = (i + (int)threadIdx.x) & (kTabCopies / 4 - 1);
+      reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = q;
+    }
+  }
 }
 
 // Sum over the 64 lanes with DPP row ops (no LDS round trips): quad swaps,
@@ -323,6 +405,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ float s_part[NW][R];
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? kTabDwords : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -355,8 +438,6 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     for (int c = threadIdx.x; c < nchunk; c += NW * 64)
       reinterpret_cast<u32x4 *>(s_x)[c] = reinterpret_cast<const u32x4 *>(p.x)[c];
   }
-  if constexpr (DQ || XL) __syncthreads();
-
   uint32_t t[8];
   if (p.lut) {  // runtime codebook -> fp16 byte tables (wave-uniform, once)
 #pragma unroll
@@ -371,6 +452,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 #pragma unroll
     for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
   }
+  if constexpr (MODE == kModeTab && (ABL & 64) == 0) build_byte_table<NW * 64>(s_tab, t);
+  if constexpr (DQ || XL || MODE == kModeTab) __syncthreads();
+  const uint32_t jb = (uint32_t)(lane & 31) << 2;
 
   float acc[R];
 #pragma unroll
@@ -391,24 +475,38 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
       else am = c.a[r];
       am = c.on ? am : 0.0f;
-      acc[r] = fmaf(chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t), am, acc[r]);
+      float d;
+      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL>(c.wv[r], hi, lo, s_tab, jb);
+      else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
+      acc[r] = fmaf(d, am, acc[r]);
     }
   };
-  // Ping-pong over two named load sets (no register copies: copying a
-  // register whose load is in flight forces vmcnt(0)).
+  // Ping-pong over two named load sets, whole pairs per iteration.  No path
+  // may consume `other` where another path consumes `cur`: hipcc would merge
+  // the two tails into one block fed by register COPIES, and copying a
+  // register whose load is in flight forces vmcnt(0) -- the prefetch is then
+  // waited for before the current step is decoded.  Every consume(cur) below
+  // reads the same registers on every path, so no copies are needed.
   if (have) {
+    const int n = (nsteps - wk + WK - 1) / WK;  // this wave's steps: s = wk, wk + WK, ...
     StepLoads<MODE, DQ, DT, R, XL, ABL> other;
-    for (;;) {
-      if (s + WK >= nsteps) { consume(cur); break; }
+    int j = 0;
+    for (; j + 2 < n; j += 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the decode
       consume(cur);
-      s += WK;
-      if (s + WK >= nsteps) { consume(other); break; }
-      cur.issue(p, row0, s + WK, lane, row_bytes);
+      cur.issue(p, row0, s + 2 * WK, lane, row_bytes);
       __builtin_amdgcn_sched_barrier(0);
       consume(other);
-      s += WK;
+      s += 2 * WK;
+    }
+    if (n - j == 2) {
+      other.issue(p, row0, s + WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(cur);
+      consume(other);
+    } else {
+      consume(cur);
     }
   }
 
@@ -526,6 +624,17 @@ static uint16_t f32_to_f16_bits(float f) {
 
 static void build_tables(int mode, int quant_type, uint32_t tab[8], float *out_scale) {
   for (int i = 0; i < 8; ++i) tab[i] = 0;
+  if (mode == kModeTab && quant_type == QZ_FP4) {
+    // 16-entry planes of the signed FP4 codebook x12: magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3}
+    // are exact fp16 values with zero low bytes; codes 8..15 carry the sign (code 8 = -0.0)
+    const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t h = (uint32_t)hb[i & 7] | (i >= 8 ? 0x80u : 0u);
+      tab[4 + (i >> 2)] |= h << (8 * (i & 3));
+    }
+    *out_scale = 1.0f / 12.0f;
+    return;
+  }
   if (mode == kModeFP4) {
     // magnitudes x12 for codes 0..7: {0, 1/16, 8, 12, 4, 6, 2, 3}, fp16 high bytes (low bytes are 0)
     const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};
@@ -583,27 +692,30 @@ static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_
 
 using namespace qz;
 
-// Geometry (WK = waves along K, R = rows per wave), from the measured sweep in
-// DESIGN.md section 4 (scripts/run_sweep2.sh on MI355X):
-//  * >= 64 Mi weights (8192x8192, 28672x8192, ...): R=4, WK=2 -- fewest
-//    redundant x/scale loads per weight byte, enough waves (>= 8 per CU);
-//  * smaller: R=2; NF4 with WK=1 (no cross-wave reduction), FP4 with WK=2;
-//  * then R halves / WK doubles until the grid has >= 2048 waves, so small-M
-//    slices (TP shards, 1024-row k/v projections) still fill the 256 CUs.
-static void choose_geometry(int M, int K, int mode, int *R, int *WK) {
+// Geometry (WK = waves along K, R = rows per wave) for the byte-table decode,
+// from the measured shape sweep in DESIGN.md section 4.1 (scripts/run24.sh):
+//  * >= 64 Mi weights (gate/up groups, 8192x28672, ...): R=4 -- more bytes in
+//    flight per wave and fewer x/scale loads per weight byte;
+//  * smaller: R=2;
+//  * WK=1 (a wave owns whole rows: no cross-wave reduction), then R halves /
+//    WK doubles until the grid has >= 2048 waves, so small-M slices (TP
+//    shards, 1024-row k/v projections) still fill the 256 CUs.
+static void choose_geometry(int M, int K, int *R, int *WK) {
   const int nsteps = ((K >> 1) + 1023) >> 10;
-  if ((long long)M * K >= (1LL << 26) && nsteps >= 2) {
-    *R = 4;
-    *WK = 2;
-  } else {
-    *R = 2;
-    *WK = (mode == kModeFP4 && nsteps >= 2) ? 2 : 1;
-  }
+  *R = ((long long)M * K >= (1LL << 26)) ? 4 : 2;
+  *WK = 1;
   while ((long long)((M + *R - 1) / *R) * (*WK) < 2048) {
     if (*R > 1) *R >>= 1;
     else if (*WK < 4 && *WK * 2 <= nsteps) *WK <<= 1;
     else break;
   }
+}
+
+// Decode tables for the byte-table kernel: the 16-entry codebook as fp16 byte
+// planes (a runtime `lut` is converted in kernel, so its planes stay zero).
+static void set_tables(int quant_type, const float *lut, uint32_t tab[8], float *out_scale) {
+  build_tables(kModeTab, lut ? QZ_NF4 : quant_type, tab, out_scale);
+  if (lut) *out_scale = 1.0f;
 }
 
 // Validates one GEMV's arguments and fills its kernel parameters (everything
@@ -668,12 +780,9 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   }
 
   int R, WK;
-  const int mode = (lut == nullptr && quant_type == QZ_FP4) ? kModeFP4 : kModeLUT16;
-  choose_geometry(M, K, mode, &R, &WK);
-  build_tables(mode, quant_type, p.tab, &p.out_scale);
-  int rc;
-  if (mode == kModeFP4) rc = dq ? dispatch_dt<kModeFP4, true>(p, dtype, R, WK, s) : dispatch_dt<kModeFP4, false>(p, dtype, R, WK, s);
-  else rc = dq ? dispatch_dt<kModeLUT16, true>(p, dtype, R, WK, s) : dispatch_dt<kModeLUT16, false>(p, dtype, R, WK, s);
+  choose_geometry(M, K, &R, &WK);
+  set_tables(quant_type, lut, p.tab, &p.out_scale);
+  const int rc = dq ? dispatch_dt<kModeTab, true>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false>(p, dtype, R, WK, s);
   if (rc != QZ_OK) return rc;
   QZ_LAUNCH_CHECK();
   return QZ_OK;
@@ -708,12 +817,11 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
     return QZ_OK;
   }
   int R, WK;
-  const int mode = (lut == nullptr && quant_type == QZ_FP4) ? kModeFP4 : kModeLUT16;
-  choose_geometry((int)total_m, K, mode, &R, &WK);
+  choose_geometry((int)total_m, K, &R, &WK);
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
-    build_tables(mode, quant_type, g.seg[i].tab, &g.seg[i].out_scale);
+    set_tables(quant_type, lut, g.seg[i].tab, &g.seg[i].out_scale);
     g.start[i] = blocks;
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }
@@ -733,8 +841,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
     else if (dtype == QZ_DT_BF16) QZ_GR_RW(MODE_, DQ_, QZ_DT_BF16); \
     else QZ_GR_RW(MODE_, DQ_, QZ_DT_F32);                     \
   } while (0)
-  if (mode == kModeFP4) { if (dq) QZ_GR_DT(kModeFP4, true); else QZ_GR_DT(kModeFP4, false); }
-  else { if (dq) QZ_GR_DT(kModeLUT16, true); else QZ_GR_DT(kModeLUT16, false); }
+  if (dq) QZ_GR_DT(kModeTab, true); else QZ_GR_DT(kModeTab, false);
 #undef QZ_GR_DT
 #undef QZ_GR_RW
 #undef QZ_GR

@@ -183,6 +183,38 @@ int main(int argc, char **argv) {
   const bool ablate = argc > 4 && std::string(argv[4]) == "ablate";
   const bool small = argc > 4 && std::string(argv[4]) == "small";
   const bool r8 = argc > 4 && std::string(argv[4]) == "r8";
+  const bool tab = argc > 4 && std::string(argv[4]) == "tab";
+  if (tab) {  // LDS byte-table decode (kModeTab = 3) vs the v_perm decode (kModeLUT16 = 1)
+    GV(1, true, 2, 1); GV(1, true, 4, 2);
+    GV(3, true, 1, 1); GV(3, true, 2, 1); GV(3, true, 4, 1); GV(3, true, 2, 2); GV(3, true, 4, 2); GV(3, true, 1, 2);
+    GVN(3, true, 2, 1, 8); GVN(3, true, 4, 2, 8); GVN(3, true, 2, 2, 8);
+  }
+  const bool tabab = argc > 4 && std::string(argv[4]) == "tabab";
+  if (tabab) {  // what bounds the table decode: 16 = no dot2c, 32 = no LDS reads, 3 = no scale/x loads, 4 = no reduction
+    GV(3, true, 2, 1); GV(3, true, 4, 2);
+    GVF(3, true, 2, 1, 4, false, 16); GVF(3, true, 4, 2, 4, false, 16);
+    GVF(3, true, 2, 1, 4, false, 32); GVF(3, true, 4, 2, 4, false, 32);
+    GVF(3, true, 2, 1, 4, false, 48); GVF(3, true, 4, 2, 4, false, 48);
+    GVF(3, true, 2, 1, 4, false, 3); GVF(3, true, 4, 2, 4, false, 3);
+    GVF(3, true, 2, 1, 4, false, 51); GVF(3, true, 4, 2, 4, false, 51);
+    GVF(2, true, 2, 1, 4, false, 3); GVF(2, true, 4, 2, 4, false, 3);
+    // 64 = no table build; mode 2 with 32 KiB of idle dynamic LDS (occupancy of the table kernel)
+    GVF(3, true, 2, 1, 4, false, 115); GVF(3, true, 4, 2, 4, false, 115);
+    GVF(3, true, 2, 1, 4, false, 64); GVF(3, true, 4, 2, 4, false, 64);
+#define GVL(MODE, DQ, R, WK, NW, ABL, LDSB) timeit("gemvL mode=" #MODE " R=" #R " WK=" #WK " NW=" #NW " ABL=" #ABL " lds=" #LDSB, [&](int i) { \
+    GemvParams q = p; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, false, ABL>), dim3(g), dim3(NW * 64), LDSB, 0, q); })
+    GVL(2, true, 2, 1, 4, 3, 32768); GVL(2, true, 4, 2, 4, 3, 32768);
+    GVL(2, true, 2, 1, 4, 3, 16384); GVL(2, true, 4, 2, 4, 3, 16384);
+  }
+  const bool tabx = argc > 4 && std::string(argv[4]) == "tabx";
+  if (tabx) {  // table decode: x traffic per weight byte (R = 8 rows per wave, x staged in LDS)
+    GV(3, true, 2, 1); GV(3, true, 4, 1); GV(3, true, 4, 2); GV(3, true, 8, 1); GV(3, true, 8, 2);
+    GVF(3, true, 2, 1, 4, true, 0); GVF(3, true, 4, 1, 4, true, 0); GVF(3, true, 4, 2, 4, true, 0);
+    GVF(3, true, 8, 1, 4, true, 0);
+    GVF(3, true, 2, 1, 8, true, 0); GVF(3, true, 4, 1, 8, true, 0); GVF(3, true, 4, 2, 8, true, 0);
+  }
   if (r8) {  // 8 rows per wave (half the x traffic per weight byte) vs the production geometries
     GV(1, true, 4, 2); GV(1, true, 2, 1); GV(1, true, 8, 1); GV(1, true, 8, 2); GV(1, true, 8, 4);
     GVN(1, true, 8, 1, 8); GVN(1, true, 8, 2, 8);
@@ -201,7 +233,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

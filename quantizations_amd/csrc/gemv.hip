@@ -58,6 +58,46 @@ enum {
 constexpr int kTabCopies = 32;
 constexpr int kTabDwords = 256 * kTabCopies;  // 32 KiB
 
+// The byte tables of the two built-in codebooks, computed at compile time and
+// stored once in device memory with each entry repeated 4 times (one 16-B
+// store per 4 bank copies): a workgroup fills its LDS image with 8 plain
+// 16-B copies per thread instead of decoding 256 entries.
+constexpr uint16_t f16_bits_rne_c(float f) {  // normal-range values and +-0 only
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  const uint32_t sign = (u >> 16) & 0x8000u, au = u & 0x7FFFFFFFu;
+  if (au == 0) return (uint16_t)sign;
+  const uint32_t e = (au >> 23) - 127u + 15u, m = au & 0x7FFFFFu;
+  uint32_t h = (e << 10) | (m >> 13);
+  const uint32_t rem = m & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h += 1u;
+  return (uint16_t)(sign | h);
+}
+struct ByteTable {
+  uint32_t v[256 * 4];
+};
+constexpr ByteTable make_byte_table(const uint16_t (&c)[16]) {
+  ByteTable t{};
+  for (int e = 0; e < 256; ++e)
+    for (int k = 0; k < 4; ++k) t.v[4 * e + k] = (uint32_t)c[e >> 4] | ((uint32_t)c[e & 15] << 16);
+  return t;
+}
+constexpr float kNF4Host[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+                                0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
+                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                                0.7229568362236023f, 1.0f};
+constexpr ByteTable make_nf4_table() {
+  uint16_t c[16] = {};
+  for (int i = 0; i < 16; ++i) c[i] = f16_bits_rne_c(kNF4Host[i]);
+  return make_byte_table(c);
+}
+// FP4 x12: magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3} (exact fp16), sign in code bit 3 (code 8 = -0.0)
+constexpr uint16_t kFP4x12Bits[16] = {0x0000, 0x2C00, 0x4800, 0x4A00, 0x4400, 0x4600, 0x4000, 0x4200,
+                                      0x8000, 0xAC00, 0xC800, 0xCA00, 0xC400, 0xC600, 0xC000, 0xC200};
+__device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
+__device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
+static_assert(f16_bits_rne_c(0.07958029955625534f) == 0x2D18, "fp16 RNE of an NF4 code");
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct GemvParams {
@@ -71,6 +111,7 @@ struct GemvParams {
   int M, K;
   int bs_log2, bs2_log2;
   float out_scale;
+  int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12) precomputed byte table; lut != nullptr builds in kernel
   uint32_t tab[8];
 };
 
@@ -120,6 +161,7 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   p.bs_log2 = keep_s(in.bs_log2);
   p.bs2_log2 = keep_s(in.bs2_log2);
   p.out_scale = keep_s(in.out_scale);
+  p.tabsel = keep_s(in.tabsel);
 #pragma unroll
   for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
   return p;
@@ -333,6 +375,19 @@ __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t
   }
 }
 
+// Fills the LDS byte table from a precomputed device table entry `v` (entry
+// e = threadIdx.x, already repeated 4 times: one 16-B store covers 4 bank
+// copies).  The 8 stores of a thread are rotated by its lane so that each
+// 8-lane store group covers all 32 banks.
+__device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u32x4 &v) {
+  const uint32_t e = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < kTabCopies / 4; ++i) {
+    const uint32_t piece = (e + (uint32_t)i) & (kTabCopies / 4 - 1);
+    reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = v;
+  }
+}
+
 // Sum over the 64 lanes with DPP row ops (no LDS round trips): quad swaps,
 // half-row and row mirrors reduce each 16-lane row, then the four row sums
 // are read back as scalars.  The result is wave-uniform.
@@ -355,7 +410,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // the inactive tail lanes of the last step read a clamped in-bounds address
 // and are zeroed at compute time, so the compiler issues every load up front
 // (no exec-masked regions, no lazily re-read kernel arguments).
-template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoads {
+template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = false> struct StepLoads {
   u32x4 wv[R];
   uint32_t q[R];    // DQ: 8-bit scale code
   float a[R];       // DQ: absmax2 entry; else: fp32 absmax
@@ -367,6 +422,10 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoa
   // loads then use the SGPR-base + 32-bit VGPR offset form, with no 64-bit
   // VALU address arithmetic per load.
   __device__ __forceinline__ void issue(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
+    if constexpr (FS) {
+      issue_full(p, row0, s, lane, row_bytes);
+      return;
+    }
     const uint32_t boff_raw = ((uint32_t)s << 10) + ((uint32_t)lane << 4);
     on = boff_raw < (uint32_t)row_bytes;
     const uint32_t boff = on ? boff_raw : 0u;
@@ -395,9 +454,41 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0> struct StepLoa
       }
     }
   }
+
+  // Full-step form (host-checked: K % 2048 == 0, K % blocksize == 0, and the
+  // step's blocks share one absmax2 entry): every lane is in range, the
+  // row's first scale block is a wave-uniform SGPR base, the lane's block
+  // offset is one VGPR shared by all R rows, and the double-quant absmax2
+  // entry of a (row, step) is ONE scalar load.
+  __device__ __forceinline__ void issue_full(const GemvParams &p, int row0, int s, int lane, int row_bytes) {
+    const uint32_t boff = ((uint32_t)s << 10) + ((uint32_t)lane << 4);
+    on = true;
+    xb = 2 * (int)boff;
+    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2u * boff);
+    const uint32_t lb = (2u * boff) >> p.bs_log2;                 // lane's block within the row
+    const uint32_t sb = ((uint32_t)s << 11) >> p.bs_log2;         // step's first block within the row
+    const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;              // blocks per row
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t row = (uint32_t)min(row0 + r, p.M - 1);  // wave-uniform
+      const unsigned char *rowp = p.B + (size_t)row * (uint32_t)row_bytes;
+      wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + boff));
+      const uint32_t rb = (uint32_t)p.block_base + row * bpr;    // wave-uniform
+      if constexpr (ABL & 1) {
+        q[r] = lb & 255u;
+        a[r] = 1.0f;
+      } else if constexpr (DQ) {
+        q[r] = (p.sc.qabsmax + rb)[lb];
+        typedef const __attribute__((address_space(4))) float *cfp;
+        a[r] = ((cfp)p.sc.absmax2)[(rb + sb) >> p.bs2_log2];
+      } else {
+        a[r] = (p.sc.absmax + rb)[lb];
+      }
+    }
+  }
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
   const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
@@ -424,8 +515,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     if (NW * 64 == 256 || threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x & 255];
     offset = *p.sc.offset;
   }
+  // 1b. the precomputed byte-table entry of this thread (issued before the
+  // weights, so waiting for it does not wait for the first HBM step)
+  u32x4 tab_entry = {0u, 0u, 0u, 0u};
+  if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
+    static_assert(NW * 64 >= 256, "one byte-table entry per thread");
+    if (!p.lut && threadIdx.x < 256)
+      tab_entry = reinterpret_cast<const u32x4 *>((p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4)->v)[threadIdx.x];
+  }
   // 2. this wave's first step of HBM traffic
-  StepLoads<MODE, DQ, DT, R, XL, ABL> cur;
+  StepLoads<MODE, DQ, DT, R, XL, ABL, FS> cur;
   int s = wk;
   cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
   const bool have = s < nsteps;
@@ -452,7 +551,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 #pragma unroll
     for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
   }
-  if constexpr (MODE == kModeTab && (ABL & 64) == 0) build_byte_table<NW * 64>(s_tab, t);
+  if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
+    if (p.lut) build_byte_table<NW * 64>(s_tab, t);
+    else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
+  }
   if constexpr (DQ || XL || MODE == kModeTab) __syncthreads();
   const uint32_t jb = (uint32_t)(lane & 31) << 2;
 
@@ -465,8 +567,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // conditional prefetch makes hipcc's waitcnt pass pick the count valid on
   // both paths -- vmcnt(0) -- which waits for the prefetch itself and
   // serialises HBM traffic with the decode.)
-  auto consume = [&](const StepLoads<MODE, DQ, DT, R, XL, ABL> &c) {
-    if constexpr (XL) const_cast<StepLoads<MODE, DQ, DT, R, XL, ABL> &>(c).xs.load_lds(s_x, c.xb);
+  auto consume = [&](const StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &c) {
+    if constexpr (XL) const_cast<StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &>(c).xs.load_lds(s_x, c.xb);
     uint32_t hi[16], lo[kSplit ? 16 : 1];
     c.xs.prepare(hi, lo);
 #pragma unroll
@@ -489,7 +591,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // reads the same registers on every path, so no copies are needed.
   if (have) {
     const int n = (nsteps - wk + WK - 1) / WK;  // this wave's steps: s = wk, wk + WK, ...
-    StepLoads<MODE, DQ, DT, R, XL, ABL> other;
+    StepLoads<MODE, DQ, DT, R, XL, ABL, FS> other;
     int j = 0;
     for (; j + 2 < n; j += 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
@@ -548,9 +650,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   }
 }
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0>
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS>(p, blockIdx.x);
 }
 
 // Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
@@ -565,7 +667,7 @@ struct GemvGroup {
   int nseg;
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK>
+template <int MODE, bool DQ, int DT, int R, int WK, bool FS>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -578,7 +680,7 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK>(seg, b - start);
+  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS>(seg, b - start);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -662,28 +764,27 @@ static int ilog2(long long v) {
   return (1LL << l) == v ? l : -1;
 }
 
-template <int MODE, bool DQ, int DT>
+// Geometries choose_geometry can return: (R, WK) in {(4,1), (2,1), (1,1), (1,2), (1,4)}.
+template <int MODE, bool DQ, int DT, bool FS>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
 #define QZ_GV(RR, WW) \
-  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW>), dim3(grid), dim3(256), 0, s, p)
-  if (WK == 4) {
-    if (R == 4) QZ_GV(4, 4); else if (R == 2) QZ_GV(2, 4); else QZ_GV(1, 4);
-  } else if (WK == 2) {
-    if (R == 4) QZ_GV(4, 2); else if (R == 2) QZ_GV(2, 2); else QZ_GV(1, 2);
-  } else {
-    if (R == 4) QZ_GV(4, 1); else if (R == 2) QZ_GV(2, 1); else QZ_GV(1, 1);
-  }
+  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS>), dim3(grid), dim3(256), 0, s, p)
+  if (R == 4) QZ_GV(4, 1);
+  else if (R == 2) QZ_GV(2, 1);
+  else if (WK == 1) QZ_GV(1, 1);
+  else if (WK == 2) QZ_GV(1, 2);
+  else QZ_GV(1, 4);
 #undef QZ_GV
 }
 
-template <int MODE, bool DQ>
+template <int MODE, bool DQ, bool FS>
 static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_t s) {
   switch (dtype) {
-    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16, FS>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16, FS>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32, FS>(p, R, WK, s); return QZ_OK;
   }
   return QZ_ERR_DTYPE;
 }
@@ -711,11 +812,22 @@ static void choose_geometry(int M, int K, int *R, int *WK) {
   }
 }
 
+// Full-step kernels (StepLoads::issue_full) need every K-step (2048 weights)
+// in range and aligned to scale blocks, and each step's blocks inside one
+// double-quant group.
+static bool full_steps(int K, int blocksize, int blocksize2, bool dq, long long block_base) {
+  if (K % 2048 != 0 || K % blocksize != 0) return false;
+  const long long step_blocks = blocksize >= 2048 ? 1 : 2048 / blocksize;
+  if (block_base % step_blocks != 0) return false;
+  return !dq || blocksize2 % step_blocks == 0;
+}
+
 // Decode tables for the byte-table kernel: the 16-entry codebook as fp16 byte
 // planes (a runtime `lut` is converted in kernel, so its planes stay zero).
-static void set_tables(int quant_type, const float *lut, uint32_t tab[8], float *out_scale) {
-  build_tables(kModeTab, lut ? QZ_NF4 : quant_type, tab, out_scale);
-  if (lut) *out_scale = 1.0f;
+static void set_tables(int quant_type, const float *lut, GemvParams *p) {
+  build_tables(kModeTab, lut ? QZ_NF4 : quant_type, p->tab, &p->out_scale);
+  p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : 0;
+  if (lut) p->out_scale = 1.0f;
 }
 
 // Validates one GEMV's arguments and fills its kernel parameters (everything
@@ -781,8 +893,12 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
 
   int R, WK;
   choose_geometry(M, K, &R, &WK);
-  set_tables(quant_type, lut, p.tab, &p.out_scale);
-  const int rc = dq ? dispatch_dt<kModeTab, true>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false>(p, dtype, R, WK, s);
+  set_tables(quant_type, lut, &p);
+  int rc;
+  if (full_steps(K, blocksize, blocksize2, dq, block_base))
+    rc = dq ? dispatch_dt<kModeTab, true, true>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false, true>(p, dtype, R, WK, s);
+  else
+    rc = dq ? dispatch_dt<kModeTab, true, false>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false, false>(p, dtype, R, WK, s);
   if (rc != QZ_OK) return rc;
   QZ_LAUNCH_CHECK();
   return QZ_OK;
@@ -821,27 +937,32 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
-    set_tables(quant_type, lut, g.seg[i].tab, &g.seg[i].out_scale);
+    set_tables(quant_type, lut, &g.seg[i]);
     g.start[i] = blocks;
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }
   for (int i = nseg; i < kMaxSeg; ++i) g.start[i] = blocks;
+  bool all_fs = true;
+  for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;
-#define QZ_GR(MODE_, DQ_, DT_, RR, WW) \
-  hipLaunchKernelGGL((k_gemv_4bit_grouped<MODE_, DQ_, DT_, RR, WW>), dim3(blocks), dim3(256), 0, s, g)
-#define QZ_GR_RW(MODE_, DQ_, DT_)                                                                   \
-  do {                                                                                            \
-    if (WK == 4) { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 4); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 4); else QZ_GR(MODE_, DQ_, DT_, 1, 4); } \
-    else if (WK == 2) { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 2); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 2); else QZ_GR(MODE_, DQ_, DT_, 1, 2); } \
-    else { if (R == 4) QZ_GR(MODE_, DQ_, DT_, 4, 1); else if (R == 2) QZ_GR(MODE_, DQ_, DT_, 2, 1); else QZ_GR(MODE_, DQ_, DT_, 1, 1); } \
+#define QZ_GR(DQ_, DT_, RR, WW, FS_) \
+  hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_>), dim3(blocks), dim3(256), 0, s, g)
+#define QZ_GR_RW(DQ_, DT_, FS_)                                      \
+  do {                                                               \
+    if (R == 4) QZ_GR(DQ_, DT_, 4, 1, FS_);                          \
+    else if (R == 2) QZ_GR(DQ_, DT_, 2, 1, FS_);                     \
+    else if (WK == 1) QZ_GR(DQ_, DT_, 1, 1, FS_);                    \
+    else if (WK == 2) QZ_GR(DQ_, DT_, 1, 2, FS_);                    \
+    else QZ_GR(DQ_, DT_, 1, 4, FS_);                                 \
   } while (0)
-#define QZ_GR_DT(MODE_, DQ_)                                  \
-  do {                                                      \
-    if (dtype == QZ_DT_F16) QZ_GR_RW(MODE_, DQ_, QZ_DT_F16);  \
-    else if (dtype == QZ_DT_BF16) QZ_GR_RW(MODE_, DQ_, QZ_DT_BF16); \
-    else QZ_GR_RW(MODE_, DQ_, QZ_DT_F32);                     \
+#define QZ_GR_DT(DQ_, FS_)                                           \
+  do {                                                               \
+    if (dtype == QZ_DT_F16) QZ_GR_RW(DQ_, QZ_DT_F16, FS_);           \
+    else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_);    \
+    else QZ_GR_RW(DQ_, QZ_DT_F32, FS_);                              \
   } while (0)
-  if (dq) QZ_GR_DT(kModeTab, true); else QZ_GR_DT(kModeTab, false);
+  if (all_fs) { if (dq) QZ_GR_DT(true, true); else QZ_GR_DT(false, true); }
+  else { if (dq) QZ_GR_DT(true, false); else QZ_GR_DT(false, false); }
 #undef QZ_GR_DT
 #undef QZ_GR_RW
 #undef QZ_GR

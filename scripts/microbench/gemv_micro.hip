@@ -215,6 +215,16 @@ int main(int argc, char **argv) {
     GVF(3, true, 8, 1, 4, true, 0);
     GVF(3, true, 2, 1, 8, true, 0); GVF(3, true, 4, 1, 8, true, 0); GVF(3, true, 4, 2, 8, true, 0);
   }
+  const bool tabfs = argc > 4 && std::string(argv[4]) == "tabfs";
+#define GVS(MODE, DQ, R, WK, NW) timeit("gemvS mode=" #MODE " dq=" #DQ " R=" #R " WK=" #WK " NW=" #NW " full-step", [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; \
+    if (DQ) { q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; } else { q.sc.absmax = A[i % NC]; } \
+    const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, false, 0, true>), dim3(g), dim3(NW * 64), 0, 0, q); })
+  if (tabfs) {  // byte-table decode: generic vs full-step loads
+    GV(3, true, 2, 1); GV(3, true, 4, 1); GVS(3, true, 2, 1, 4); GVS(3, true, 4, 1, 4);
+    GVS(3, true, 1, 1, 4); GVS(3, true, 2, 1, 8); GVS(3, true, 4, 1, 8); GVS(3, false, 2, 1, 4); GVS(3, false, 4, 1, 4);
+  }
   if (r8) {  // 8 rows per wave (half the x traffic per weight byte) vs the production geometries
     GV(1, true, 4, 2); GV(1, true, 2, 1); GV(1, true, 8, 1); GV(1, true, 8, 2); GV(1, true, 8, 4);
     GVN(1, true, 8, 1, 8); GVN(1, true, 8, 2, 8);
@@ -233,7 +243,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

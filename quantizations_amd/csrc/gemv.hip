@@ -523,6 +523,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     if (!p.lut && threadIdx.x < 256)
       tab_entry = reinterpret_cast<const u32x4 *>((p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4)->v)[threadIdx.x];
   }
+  // 1c. XL: this thread's share of x (<= kXLChunks 16-B chunks), also ahead of the weights
+  constexpr int kXLChunks = XL ? 8 : 1;
+  u32x4 xr[kXLChunks];
+  const int x_nchunk = (p.K * XB) >> 4;
+  if constexpr (XL) {
+#pragma unroll
+    for (int i = 0; i < kXLChunks; ++i) {
+      const int c = (int)threadIdx.x + i * NW * 64;
+      if (c < x_nchunk) xr[i] = reinterpret_cast<const u32x4 *>(p.x)[c];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // 2. this wave's first step of HBM traffic
   StepLoads<MODE, DQ, DT, R, XL, ABL, FS> cur;
   int s = wk;
@@ -532,10 +544,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   if constexpr (DQ) {
     if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
   }
-  if constexpr (XL) {  // x -> LDS, 16 B per thread per pass
-    const int nchunk = (p.K * XB) >> 4;
-    for (int c = threadIdx.x; c < nchunk; c += NW * 64)
-      reinterpret_cast<u32x4 *>(s_x)[c] = reinterpret_cast<const u32x4 *>(p.x)[c];
+  if constexpr (XL) {  // x -> LDS (the launcher guarantees K * XB <= kXLChunks * 16 * NW * 64)
+#pragma unroll
+    for (int i = 0; i < kXLChunks; ++i) {
+      const int c = (int)threadIdx.x + i * NW * 64;
+      if (c < x_nchunk) reinterpret_cast<u32x4 *>(s_x)[c] = xr[i];
+    }
   }
   uint32_t t[8];
   if (p.lut) {  // runtime codebook -> fp16 byte tables (wave-uniform, once)

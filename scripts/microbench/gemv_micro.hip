@@ -221,6 +221,15 @@ int main(int argc, char **argv) {
     if (DQ) { q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; } else { q.sc.absmax = A[i % NC]; } \
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, QZ_DT_F16, R, WK, NW, false, 0, true>), dim3(g), dim3(NW * 64), 0, 0, q); })
+#define GVX(MODE, R, WK, NW) timeit("gemvX mode=" #MODE " R=" #R " WK=" #WK " NW=" #NW " full-step x-in-LDS", [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<MODE, true, QZ_DT_F16, R, WK, NW, true, 0, true>), dim3(g), dim3(NW * 64), K * 2, 0, q); })
+  const bool tabxl = argc > 4 && std::string(argv[4]) == "tabxl";
+  if (tabxl) {
+    GVS(3, true, 2, 1, 4); GVS(3, true, 4, 1, 4); GVX(3, 2, 1, 4); GVX(3, 4, 1, 4); GVX(3, 1, 1, 4);
+    GVX(3, 2, 1, 8); GVX(3, 4, 1, 8); GVX(3, 1, 1, 8); GVX(3, 2, 2, 8);
+  }
   if (tabfs) {  // byte-table decode: generic vs full-step loads
     GV(3, true, 2, 1); GV(3, true, 4, 1); GVS(3, true, 2, 1, 4); GVS(3, true, 4, 1, 4);
     GVS(3, true, 1, 1, 4); GVS(3, true, 2, 1, 8); GVS(3, true, 4, 1, 8); GVS(3, false, 2, 1, 4); GVS(3, false, 4, 1, 4);
@@ -243,7 +252,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

@@ -1,8 +1,9 @@
-# ablations of the LDS byte-table GEMV decode
+# GEMV microbench runs: MODE selects the variant set, SHAPES lists M_K pairs
 set -u
 cd $GRAFT_REPO_ROOT/scripts/microbench
-for s in ${SHAPES:-"4096 4096" "28672 4096" "8192 28672"}; do
-  timeout -k 10 120 ./gemv_micro $s 7 ${MODE:-tabab} > ../../gpurun_out/tabab_${s// /x}.log 2>&1; rc=$?
-  echo "== $s rc=$rc"; grep -v "^floor T=256 L=1" ../../gpurun_out/tabab_${s// /x}.log
+for sh in ${SHAPES:-4096_4096 28672_4096 8192_28672}; do
+  s=${sh//_/ }
+  timeout -k 10 120 ./gemv_micro $s 7 ${MODE:-tabab} > ../../gpurun_out/mb_${MODE:-tabab}_${sh}.log 2>&1; rc=$?
+  echo "== $s rc=$rc"; grep -v "^floor T=256 L=1" ../../gpurun_out/mb_${MODE:-tabab}_${sh}.log
   [ $rc -eq 0 ] || exit $rc
 done

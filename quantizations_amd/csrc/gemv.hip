@@ -356,6 +356,22 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
   return s0 + s1;
 }
 
+// Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
+// (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
+// readlane round trips through SGPRs.
+template <int CTRL, int ROWS> __device__ __forceinline__ float dpp_add_rows(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_last(float v) {
+  v = dpp_add_rows<0x111, 0xF>(v);  // row_shr:1
+  v = dpp_add_rows<0x112, 0xF>(v);  // row_shr:2
+  v = dpp_add_rows<0x114, 0xF>(v);  // row_shr:4
+  v = dpp_add_rows<0x118, 0xF>(v);  // row_shr:8
+  v = dpp_add_rows<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  v = dpp_add_rows<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+  return v;
+}
+
 // Builds the kModeTab byte table from the 16-entry fp16 byte planes t[8]
 // (every thread of the workgroup takes part; the caller synchronises).
 template <int NT>
@@ -378,7 +394,9 @@ __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t
 // Fills the LDS byte table from a precomputed device table entry `v` (entry
 // e = threadIdx.x, already repeated 4 times: one 16-B store covers 4 bank
 // copies).  The 8 stores of a thread are rotated by its lane so that each
-// 8-lane store group covers all 32 banks.
+// 8-lane store group covers all 32 banks.  (Loading 8 pieces per thread to
+// make every store address an immediate offset was measured slower: the
+// extra loads delay the first weight loads.)
 __device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u32x4 &v) {
   const uint32_t e = threadIdx.x;
 #pragma unroll
@@ -386,24 +404,6 @@ __device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u3
     const uint32_t piece = (e + (uint32_t)i) & (kTabCopies / 4 - 1);
     reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = v;
   }
-}
-
-// Sum over the 64 lanes with DPP row ops (no LDS round trips): quad swaps,
-// half-row and row mirrors reduce each 16-lane row, then the four row sums
-// are read back as scalars.  The result is wave-uniform.
-template <int CTRL> __device__ __forceinline__ float dpp_add(float v) {
-  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float wave_sum(float v) {
-  v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
-  v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
-  v = dpp_add<0x141>(v);  // row_half_mirror
-  v = dpp_add<0x140>(v);  // row_mirror
-  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-  return (r0 + r1) + (r2 + r3);
 }
 
 // One step's worth of loads for R rows.  Branch-free: out-of-range rows and
@@ -517,6 +517,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   }
   // 1b. the precomputed byte-table entry of this thread (issued before the
   // weights, so waiting for it does not wait for the first HBM step)
+  // 1b. the precomputed byte-table entry of this thread (issued before the
+  // weights, so waiting for it does not wait for the first HBM step)
   u32x4 tab_entry = {0u, 0u, 0u, 0u};
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
@@ -569,7 +571,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     if (p.lut) build_byte_table<NW * 64>(s_tab, t);
     else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
   }
-  if constexpr (DQ || XL || MODE == kModeTab) __syncthreads();
+  if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
   const uint32_t jb = (uint32_t)(lane & 31) << 2;
 
   float acc[R];
@@ -631,23 +633,27 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
     return;
   }
-  if constexpr (WK == 1) {  // the wave owns whole rows: no cross-wave pass
+  if constexpr (WK == 1) {  // the wave owns whole rows: lane 63 reduces and stores them
+    float v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float v = (ABL & 8) ? acc[r] : wave_sum(acc[r]);
-      const int row = row0 + r;
-      if (lane == r && row < p.M) {
-        float o = v * p.out_scale;
-        if (p.bias) o += load_f32<DT>(p.bias, row);
-        store_f32<DT>(p.y, row, o);
+    for (int r = 0; r < R; ++r) v[r] = (ABL & 8) ? acc[r] : wave_sum_last(acc[r]);
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        if (row < p.M) {
+          float o = v[r] * p.out_scale;
+          if (p.bias) o += load_f32<DT>(p.bias, row);
+          store_f32<DT>(p.y, row, o);
+        }
       }
     }
     return;
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float v = (ABL & 8) ? acc[r] : wave_sum(acc[r]);
-    if (lane == 0) s_part[wave][r] = v;
+    const float v = (ABL & 8) ? acc[r] : wave_sum_last(acc[r]);
+    if (lane == kWave - 1) s_part[wave][r] = v;
   }
   __syncthreads();
   if ((int)threadIdx.x < RG * R) {
@@ -724,8 +730,8 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_generic(GemvParams p, int qua
     else c = (nib & 8u ? -1.0f : 1.0f) * dequant_fp4_tree(nib & 7u, 1.0f);
     acc = fmaf(load_f32<DT>(p.x, k), __fmul_rn(c, am), acc);
   }
-  acc = wave_sum(acc);
-  if (lane == 0) {
+  acc = wave_sum_last(acc);
+  if (lane == kWave - 1) {
     if (p.bias) acc += load_f32<DT>(p.bias, row);
     store_f32<DT>(p.y, row, acc);
   }

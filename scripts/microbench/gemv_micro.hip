@@ -66,9 +66,9 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit_sl(GemvParams p_in) {
 
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float v = wave_sum(acc[r]);
+    const float v = wave_sum_last(acc[r]);
     const int row = row0 + r;
-    if (lane == r && row < p.M) {
+    if (lane == kWave - 1 && row < p.M) {
       float o = v * p.out_scale;
       if (p.bias) o += load_f32<DT>(p.bias, row);
       store_f32<DT>(p.y, row, o);
@@ -234,6 +234,16 @@ int main(int argc, char **argv) {
     GV(3, true, 2, 1); GV(3, true, 4, 1); GVS(3, true, 2, 1, 4); GVS(3, true, 4, 1, 4);
     GVS(3, true, 1, 1, 4); GVS(3, true, 2, 1, 8); GVS(3, true, 4, 1, 8); GVS(3, false, 2, 1, 4); GVS(3, false, 4, 1, 4);
   }
+  const bool skel = argc > 4 && std::string(argv[4]) == "skel";
+  if (skel) {  // what the GEMV skeleton costs over a bare streaming read
+    // 7: loads only; 3: + DPP reduction + store; 11: + store without reduction; 259: + lane-63 reduction + store
+    GVF(2, false, 2, 1, 4, false, 7); GVF(2, false, 2, 1, 4, false, 3); GVF(2, false, 2, 1, 4, false, 11);
+    GVF(2, false, 2, 1, 4, false, 259);
+    // table kernel: 115 = no decode work at all; +128 = no prologue barrier; +256 = lane-63 reduction
+    GVF(3, false, 2, 1, 4, false, 115); GVF(3, false, 2, 1, 4, false, 243); GVF(3, false, 2, 1, 4, false, 371);
+    GVF(3, true, 2, 1, 4, false, 0); GVF(3, true, 2, 1, 4, false, 256);
+    GVS(3, true, 2, 1, 4);
+  }
   if (r8) {  // 8 rows per wave (half the x traffic per weight byte) vs the production geometries
     GV(1, true, 4, 2); GV(1, true, 2, 1); GV(1, true, 8, 1); GV(1, true, 8, 2); GV(1, true, 8, 4);
     GVN(1, true, 8, 1, 8); GVN(1, true, 8, 2, 8);
@@ -252,7 +262,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

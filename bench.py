@@ -15,8 +15,12 @@ config #1 CPU dequant+matmul baseline.
   pairing -- q/k/v and gate/up column-parallel (rank p keeps its heads / MLP
   columns as row slices of the global quant state), o_proj and down_proj
   row-parallel (input-column slices) + one RCCL all-reduce each: 2 collectives
-  per layer.  --tp-mode gather: every Linear4bit row-split + all-gather.  The
-  same single decode stream is served by all N GPUs (strong scaling).
+  per layer.  --tp-mode gather: every Linear4bit row-split + all-gather.
+  Weak scaling (default): each GPU adds one bs=1 decode stream (global batch
+  N) and every layer is sharded over all N GPUs, so each GPU streams 1/N of
+  the weights once per step for N tokens -- per-GPU work fixed.  --strong:
+  one bs=1 stream served by all N GPUs (config #5's literal layout; latency-
+  bound on the collectives at bs=1).
 * roofline: the 4096x4096 NF4+DQ fused GEMV alone, 64 rotating weight copies
   (> the 256 MiB Infinity Cache), HIP events on the launch stream around 400
   back-to-back launches (average launch duration, matches rocprofv3);
@@ -81,12 +85,12 @@ def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_typ
 
 
 @torch.inference_mode()
-def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: int):
+def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: int, batch: int = 1):
     from transformers.cache_utils import DynamicCache
 
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1234)
-    ids = torch.randint(0, cfg.vocab_size, (1, prompt_len), generator=g).to(dev)
+    ids = torch.randint(0, cfg.vocab_size, (batch, prompt_len), generator=g).to(dev)
     cache = DynamicCache()
     out = model(input_ids=ids, past_key_values=cache, use_cache=True)      # prefill (fused MFMA GEMM path)
     nxt = out.logits[:, -1:].argmax(-1)
@@ -110,28 +114,29 @@ def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: in
 
 
 @torch.inference_mode()
-def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int):
+def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int, batch: int = 1):
     """Same workload as decode_bench, with the decode step captured once into a HIP
     graph (StaticCache, static token/position buffers; the graph contains the
     whole forward, the argmax and the feedback of the token into the next
-    step).  One replay = one generated token."""
+    step).  One replay = one generated token per stream (`batch` streams)."""
     from transformers.cache_utils import StaticCache
 
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1234)
-    ids = torch.randint(0, cfg.vocab_size, (1, prompt_len), generator=g).to(dev)
+    ids = torch.randint(0, cfg.vocab_size, (batch, prompt_len), generator=g).to(dev)
     cache = StaticCache(config=cfg, max_cache_len=prompt_len + warmup + steps + 8)
     out = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(prompt_len, device=dev),
                 use_cache=True)
     tok = out.logits[:, -1:].argmax(-1)
     pos = torch.tensor([prompt_len], device=dev, dtype=torch.long)
-    hist = torch.zeros((1, prompt_len + warmup + steps + 8), device=dev, dtype=torch.long)
+    hist = torch.zeros((batch, prompt_len + warmup + steps + 8), device=dev, dtype=torch.long)
+    pos_ids = pos.view(1, 1).expand(batch, 1)
 
     def step():
-        lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos.view(1, 1),
+        lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos_ids,
                    use_cache=True).logits
         nxt = lo[:, -1:].argmax(-1)
-        hist.index_copy_(1, pos, nxt.view(1, 1))
+        hist.index_copy_(1, pos, nxt.view(batch, 1))
         tok.copy_(nxt)
         pos.add_(1)
 
@@ -231,7 +236,76 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(floor)
     floor_us = e0.elapsed_time(e1) * 1e3 / iters
-    return statistics.mean(us), statistics.median(us), b2b_us, floor_us
+
+    # the fixed back-to-back period of an EMPTY dependent launch (same method): the
+    # part of every launch's duration that moves no bytes
+    empty_fn = _lib.lib.qz_bench_empty
+
+    def empty():
+        e0.record()
+        for _ in range(iters):
+            rc = empty_fn(sink.data_ptr(), stream)
+            if rc:
+                raise RuntimeError(f"qz_bench_empty rc={rc}")
+        e1.record()
+
+    blocked(empty)
+    empty_us = e0.elapsed_time(e1) * 1e3 / iters
+    return statistics.mean(us), statistics.median(us), b2b_us, floor_us, empty_us
+
+
+def gemv_alg_bytes(shapes, dq: bool = True, x_bytes: int = 2, y_bytes: int = 2) -> int:
+    """Algorithmic bytes of one (grouped) NF4 decode GEMV launch:
+    per segment packed M*K/2 + scales (u8 codes + fp32 absmax2/256 + offset +
+    code2, or fp32 absmax) + x + y, plus the 16-entry codebook once."""
+    total = 64
+    for m, k in shapes:
+        n = m * k
+        total += n // 2 + x_bytes * k + y_bytes * m
+        total += (n // 64 + 4 * (n // 64 // 256) + 4 + 1024) if dq else 4 * (n // 64)
+    return total
+
+
+assert gemv_alg_bytes([(4096, 4096)]) == GEMV_BYTES_4096
+
+
+@torch.inference_mode()
+def dominant_roofline(copies: int = 8, iters: int = 100):
+    """The decode step's longest Linear4bit launch: the grouped gate/up GEMV of a
+    Llama-3-8B layer (2 x 14336x4096 NF4+DQ in ONE launch), rotating weights
+    (8 sets = 485 MB > the 256 MiB Infinity Cache), same timing method."""
+    from quantizations_amd.core import gemv_4bit_grouped, quantize_4bit
+
+    dev = torch.device("cuda")
+    torch.manual_seed(8)
+    sets = []
+    for _ in range(copies):
+        items = []
+        for _ in range(2):
+            W = (torch.randn(14336, 4096, device=dev) * 0.02).to(torch.float16)
+            packed, qs = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+            items.append((packed, qs, None))
+        sets.append(items)
+        del W
+    x = torch.randn(1, 1, 4096, device=dev).to(torch.float16)
+    outs = [torch.empty(14336, device=dev, dtype=torch.float16) for _ in range(2)]
+    sets = [[(p, q, b, 0, o) for (p, q, b), o in zip(items, outs)] for items in sets]
+    for i in range(2 * copies):
+        gemv_4bit_grouped(x, sets[i % copies])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(100_000_000)
+    e0.record()
+    for i in range(iters):
+        gemv_4bit_grouped(x, sets[i % copies])
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    nbytes = gemv_alg_bytes([(14336, 4096)] * 2)
+    return {"kernel": "k_gemv_4bit_grouped gate/up 2 x 14336x4096 NF4+DQ (one launch per layer)",
+            "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
+            "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 @torch.inference_mode()
@@ -368,6 +442,10 @@ def main():
                          "layer) or row-split every Linear4bit + all-gather")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the multi-GPU code path (process group, sharded layers, RCCL) even at world size 1")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="decode streams per GPU (bs=1 each); the global batch is batch x N (weak scaling)")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: keep the global batch at --batch (one bs=1 stream served by all N GPUs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -381,9 +459,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     if args.gemv_only:
-        mean_us, med_us, b2b_us, floor_us = gemv_roofline()
+        mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         print(json.dumps({"gemv_4096_us_mean": mean_us, "gemv_4096_us_median": med_us, "back_to_back_us": b2b_us,
-                          "read_floor_us": floor_us,
+                          "read_floor_us": floor_us, "empty_launch_us": empty_us,
                           "achieved_GBs": GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9}), flush=True)
         return
 
@@ -414,27 +492,31 @@ def main():
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 
+    # Weak scaling (default): every GPU adds one bs=1 decode stream and every
+    # Linear4bit is sharded over all N GPUs (TP), so per-GPU work -- weight bytes
+    # x tokens -- stays fixed as N grows.  --strong: one global batch for any N.
+    gbatch = args.batch if (args.strong or not sharded) else args.batch * world
     mode = "eager"
     if not args.eager:
         try:
-            dt, toks = decode_bench_graph(model, cfg, args.steps, args.warmup, args.prompt, world)
+            dt, toks = decode_bench_graph(model, cfg, args.steps, args.warmup, args.prompt, world, gbatch)
             mode = "hipgraph"
         except Exception as e:  # capture unsupported by this transformers build -> eager
             log(f"[rank {rank}] graph decode failed ({type(e).__name__}: {e}); falling back to eager")
             torch.cuda.synchronize()
     if mode == "eager":
-        dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world)
+        dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world, gbatch)
     t = torch.tensor([dt], device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    tok_s = args.steps / dt
+    tok_s = args.steps * gbatch / dt   # tokens generated by all streams, whole job
 
     roof = None
     if rank == 0 and not args.no_roofline:
         del model
         torch.cuda.empty_cache()
-        mean_us, med_us, b2b_us, floor_us = gemv_roofline()
+        mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         # average launch duration = HIP events around `iters` back-to-back launches on
         # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
         # overhead on ROCm and disagrees with rocprofv3, so it is reported only.
@@ -450,7 +532,13 @@ def main():
                 "launch_us_avg": round(b2b_us, 3),
                 "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
                 "one_shot_read_floor_us": round(floor_us, 3),
-                "frac_of_one_shot_floor": round(floor_us / b2b_us, 4)}
+                "frac_of_one_shot_floor": round(floor_us / b2b_us, 4),
+                # what one launch can reach at all: an empty dependent launch's period
+                # plus the 8.67 MB at peak bandwidth
+                "empty_launch_us": round(empty_us, 3),
+                "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
+                                                                    * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "dominant_decode_kernel": dominant_roofline()}
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:
@@ -465,11 +553,12 @@ def main():
             "metric": "decode tokens/sec Llama-3-8B NF4 bs=1; 4096×4096 GEMV GB/s vs HBM peak",
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
+            "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}-decode-bs1",
                        "layers": cfg.num_hidden_layers,
-                       "prompt_len": args.prompt, "batch": 1, "decode": mode,
+                       "prompt_len": args.prompt, "global_batch": gbatch, "streams_per_gpu": gbatch / world,
+                       "stream_batch": 1, "decode": mode,
                        "parallelism": ("single" if not sharded else
                                        f"tp{world}-megatron-pair-allreduce" if args.tp_mode == "pair" else
                                        f"tp{world}-rowsplit-allgather"),

@@ -182,6 +182,10 @@ int qz_dequantize_4bit(const unsigned char *A, long long n, int quant_type, int 
  * one-shot HBM read floor of a buffer the GEMV's size. */
 int qz_bench_read_floor(const void *p, long long bytes, unsigned int *sink, void *stream);
 
+/* Measurement helper: one empty 64-thread launch -- the fixed back-to-back
+ * period every dependent launch on a stream pays (dispatch + end of kernel). */
+int qz_bench_empty(unsigned int *sink, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

@@ -64,6 +64,7 @@ SIGNATURES = {
     "qz_dequantize_blockwise_8bit": [_p, _p, _p, _ll, _i, _p, _p, _p],
     "qz_dequantize_4bit": [_p, _ll, _i, _i, _p, _p, _p, _p, _p, _i, _p, _i, _p],
     "qz_bench_read_floor": [_p, _ll, _p, _p],
+    "qz_bench_empty": [_p, _p],
     "qz_version": [],
 }
 RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll}

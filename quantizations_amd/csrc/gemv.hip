@@ -142,6 +142,38 @@ template <typename T> __device__ __forceinline__ T *keep_sp(T *v) {
   return (T *)g;
 }
 
+// Diagnostic timeline stamps (dev builds only: scripts/microbench defines
+// QZ_STAMPS and instantiates ABL & 512).  The product library compiles none of
+// this.  Per wave: s_memrealtime (100 MHz, chip-wide) at fixed points, stored
+// once at the end by lane 0 with the wave's XCC / HW ids.
+#ifdef QZ_STAMPS
+__device__ unsigned long long *g_qz_stamp;
+#define QZ_STAMP_DECL unsigned long long qz_st_[6] = {0, 0, 0, 0, 0, 0}
+#define QZ_STAMP(k)                                                                  \
+  do {                                                                               \
+    if constexpr ((ABL & 512) != 0) {                                                \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(qz_st_[k])::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                             \
+    }                                                                                \
+  } while (0)
+#define QZ_STAMP_FLUSH(wave_id)                                                      \
+  do {                                                                               \
+    if constexpr ((ABL & 512) != 0) {                                                \
+      uint32_t xcc, hw;                                                              \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));             \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));               \
+      qz_st_[5] = ((unsigned long long)xcc << 32) | hw;                              \
+      if ((threadIdx.x & 63) == 0)                                                   \
+        for (int k_ = 0; k_ < 6; ++k_) g_qz_stamp[(size_t)(wave_id) * 8 + k_] = qz_st_[k_]; \
+    }                                                                                \
+  } while (0)
+#else
+#define QZ_STAMP_DECL
+#define QZ_STAMP(k) do {} while (0)
+#define QZ_STAMP_FLUSH(wave_id) do {} while (0)
+#endif
+
 __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   GemvParams p;
   p.B = keep_sp(in.B);
@@ -490,6 +522,8 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
+  QZ_STAMP_DECL;
+  QZ_STAMP(0);
   const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
   constexpr bool kSplit = DT != QZ_DT_F16;
@@ -572,6 +606,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
   }
   if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
+  QZ_STAMP(1);
   const uint32_t jb = (uint32_t)(lane & 31) << 2;
 
   float acc[R];
@@ -622,6 +657,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       other.issue(p, row0, s + WK, lane, row_bytes);
       __builtin_amdgcn_sched_barrier(0);
       consume(cur);
+      QZ_STAMP(2);
       consume(other);
     } else {
       consume(cur);
@@ -633,6 +669,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
     return;
   }
+  QZ_STAMP(3);
   if constexpr (WK == 1) {  // the wave owns whole rows: lane 63 reduces and stores them
     float v[R];
 #pragma unroll
@@ -648,6 +685,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
         }
       }
     }
+    QZ_STAMP(4);
+    QZ_STAMP_FLUSH(block * NW + wave);
     return;
   }
 #pragma unroll

@@ -3,6 +3,7 @@
 // so the 256 MiB Infinity Cache never serves repeats.  Run under
 // `rocprofv3 --kernel-trace --stats` for kernel-only durations; the printed
 // numbers are hipEvent back-to-back averages (kernel + launch gap).
+#define QZ_STAMPS 1
 #include "../../quantizations_amd/csrc/gemv.hip"
 
 namespace qz {
@@ -117,6 +118,31 @@ __global__ __launch_bounds__(T) void k_read_floor_store(const unsigned char *__r
     }
   }
   if ((threadIdx.x & 63) < 2) out[(blockIdx.x * T + threadIdx.x) / 32] = acc;  // 2 rows' worth per wave
+}
+
+// one-shot floor with timeline stamps (start, data back, end) per wave
+__global__ __launch_bounds__(256) void k_floor_stamp(const unsigned char *__restrict__ p, long long bytes, uint32_t *sink) {
+  unsigned long long t0, t1;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  const long long c = (long long)blockIdx.x * 256 + threadIdx.x;
+  v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p) + (c < bytes / 16 ? c : 0));
+  uint32_t acc = v.x ^ v.y ^ v.z ^ v.w;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  if (acc == 0x12345678u) sink[0] = acc;
+  uint32_t xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long *o = qz::g_qz_stamp + (size_t)(blockIdx.x * 4 + threadIdx.x / 64) * 8;
+    o[0] = t0; o[1] = t1; o[2] = t1; o[3] = t1; o[4] = t1; o[5] = ((unsigned long long)xcc << 32) | hw;
+  }
+}
+
+// park the stream (~20 ms) so the host has enqueued a whole round before the GPU reaches it
+__global__ void k_spin(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
 }
 
 // random packed weights (a constant fill would make every LDS lookup a broadcast)
@@ -244,6 +270,17 @@ int main(int argc, char **argv) {
     GVF(3, true, 2, 1, 4, false, 0); GVF(3, true, 2, 1, 4, false, 256);
     GVS(3, true, 2, 1, 4);
   }
+  const bool tabab2 = argc > 4 && std::string(argv[4]) == "tabab2";
+#define GVFS(R, ABL) timeit("gemvFS tab dq R=" #R " ABL=" #ABL, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, ABL, true>), dim3(g), dim3(256), 0, 0, q); })
+  if (tabab2) {  // full-step table kernel ablations: 1 no scale loads, 2 no x loads, 4 no reduce/store,
+                 // 8 no DPP reduction, 16 no dots, 32 no LDS reads, 64 no table build, 128 no prologue barrier
+    GVFS(2, 0); GVFS(2, 1); GVFS(2, 2); GVFS(2, 3); GVFS(2, 4); GVFS(2, 16); GVFS(2, 32); GVFS(2, 48);
+    GVFS(2, 112); GVFS(2, 115); GVFS(2, 119); GVFS(2, 2 + 16 + 32);
+    GVFS(4, 0); GVFS(4, 2); GVFS(4, 3); GVFS(1, 0); GVFS(1, 2);
+  }
   if (r8) {  // 8 rows per wave (half the x traffic per weight byte) vs the production geometries
     GV(1, true, 4, 2); GV(1, true, 2, 1); GV(1, true, 8, 1); GV(1, true, 8, 2); GV(1, true, 8, 4);
     GVN(1, true, 8, 1, 8); GVN(1, true, 8, 2, 8);
@@ -262,7 +299,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
@@ -283,11 +320,68 @@ int main(int argc, char **argv) {
   if (nsw == 7) { SL(0, 2, 7); SL(0, 4, 7); }
   if (nsw == 14) { SL(0, 2, 14); SL(0, 4, 14); }
   }
+  const bool stamps = argc > 4 && std::string(argv[4]) == "stamps";
+  if (stamps) {  // timeline of one steady-state launch (the last of 30 back-to-back), 12 samples each
+    const int NWAVES = 1 << 16;
+    unsigned long long *sbuf;
+    CK(hipMalloc(&sbuf, (size_t)NWAVES * 8 * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_qz_stamp), &sbuf, sizeof(sbuf)));
+    std::vector<unsigned long long> h((size_t)NWAVES * 8);
+    auto run = [&](const char *name, int nwaves, std::function<void(int)> launch) {
+      printf("== stamps: %s (%d waves); us from the first wave's start\n", name, nwaves);
+      printf("   start p50/p90/max | t1 p50/p90/max | t2 p50/p90/max | t3 p50/max | end p50/p90/max\n");
+      for (int smp = 0; smp < 12; ++smp) {
+        hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, 0, 200000LL);
+        for (int i = 0; i < 30; ++i) launch(smp * 30 + i);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(h.data(), sbuf, (size_t)nwaves * 64, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull;
+        for (int w = 0; w < nwaves; ++w) t0 = std::min(t0, h[(size_t)w * 8]);
+        std::vector<double> c[5];
+        for (int w = 0; w < nwaves; ++w)
+          for (int k = 0; k < 5; ++k) c[k].push_back((h[(size_t)w * 8 + k] - t0) * 0.01);
+        for (int k = 0; k < 5; ++k) std::sort(c[k].begin(), c[k].end());
+        auto q = [&](int k, double f) { return c[k][std::min((size_t)(f * nwaves), (size_t)nwaves - 1)]; };
+        printf("   %5.2f %5.2f %5.2f | %5.2f %5.2f %5.2f | %5.2f %5.2f %5.2f | %5.2f %5.2f | %5.2f %5.2f %5.2f\n",
+               q(0, .5), q(0, .9), q(0, 1), q(1, .5), q(1, .9), q(1, 1), q(2, .5), q(2, .9), q(2, 1), q(3, .5), q(3, 1),
+               q(4, .5), q(4, .9), q(4, 1));
+        if (smp == 11) {  // per-XCC start / end medians of the last sample
+          for (int x = 0; x < 8; ++x) {
+            std::vector<double> s0, s4;
+            for (int w = 0; w < nwaves; ++w)
+              if ((int)(h[(size_t)w * 8 + 5] >> 32) == x) {
+                s0.push_back((h[(size_t)w * 8] - t0) * 0.01);
+                s4.push_back((h[(size_t)w * 8 + 4] - t0) * 0.01);
+              }
+            if (s0.empty()) continue;
+            std::sort(s0.begin(), s0.end()); std::sort(s4.begin(), s4.end());
+            printf("   xcc %d: %zu waves, start med %.2f max %.2f, end med %.2f max %.2f\n", x, s0.size(),
+                   s0[s0.size() / 2], s0.back(), s4[s4.size() / 2], s4.back());
+          }
+        }
+      }
+    };
+    {
+      const long long nchunk = pbytes / 16;
+      const unsigned g = (unsigned)((nchunk + 255) / 256);
+      run("floor T=256 L=1", g * 4, [&](int i) {
+        hipLaunchKernelGGL(k_floor_stamp, dim3(g), dim3(256), 0, 0, P[i % NC], (long long)pbytes, sink); });
+    }
+    {
+      const int R = 2;
+      const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4));
+      run("gemv tab DQ R=2 full-step", g * 4, [&, pt = p](int i) {
+        GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC];
+        hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true>), dim3(g), dim3(256), 0, 0, q); });
+    }
+    return 0;
+  }
   const int ROUNDS = argc > 3 ? atoi(argv[3]) : 9;
   for (auto &v : vs) { for (int i = 0; i < NC; ++i) v.launch(i); }
   CK(hipDeviceSynchronize());
   for (int r = 0; r < ROUNDS; ++r)
     for (auto &v : vs) {
+      hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, 0, 2000000LL);  // host enqueues the round meanwhile
       CK(hipEventRecord(e0));
       for (int i = 0; i < ITERS; ++i) v.launch(i);
       CK(hipEventRecord(e1));

@@ -191,7 +191,7 @@ def _tp_hook(x, mod):
     return y.to(x.dtype)
 
 
-def _tp_worker(rank, world, port, q):
+def _tp_worker(rank, world, port, q, batch=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -233,7 +233,7 @@ def _tp_worker(rank, world, port, q):
             ref.get_submodule(name).weight.data.copy_(torch.from_numpy(oracle.dequantize(st)).reshape(M, K))
         n = apply_tensor_parallel(model, rank, world, local_matmul=_tp_hook)
         groups = fuse_projection_groups(model)
-        ids = torch.tensor([[5, 17, 3, 88, 41, 9]])
+        ids = torch.tensor([[5, 17, 3, 88, 41, 9], [7, 2, 60, 11, 4, 30]])[:batch]
         with torch.no_grad():
             ref_logits = ref(input_ids=ids).logits
             out = model(input_ids=ids, use_cache=True)
@@ -250,17 +250,19 @@ def _tp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_tensor_parallel_pairing_tiny_llama():
+@pytest.mark.parametrize("batch", [1, 2])
+def test_tensor_parallel_pairing_tiny_llama(batch):
     """Megatron TP pairing (column q/k/v/gate/up, row o/down + all-reduce) on a
     tiny Llama over gloo world 2: logits of prefill and of a cached decode step
-    equal the unsharded model's (fp32 sums in another order)."""
+    equal the unsharded model's (fp32 sums in another order).  batch 2 is the
+    bench's weak-scaling layout (one decode stream per GPU, TP over all GPUs)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
         os.environ.get("PYTHONPATH", "")
-    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, batch)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]

@@ -145,6 +145,15 @@ int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dtype, const u
                  const float *code2, const float *offset, int blocksize2, const void *bias, void *Y, int ldy,
                  float *workspace, long long workspace_bytes, void *stream);
 
+/* Grouped multi-token GEMM (2 <= T <= 16 tokens, K % 256 == 0): the batched-
+ * decode counterpart of qz_gemv_4bit_grouped -- segments that share X (e.g.
+ * q/k/v or gate/up of one layer over a small batch) in ONE launch.  Segment
+ * i writes y_i[T, M_i] (row stride M_i); every output is bit-identical to
+ * qz_gemm_4bit on that segment alone (block_base as in qz_gemv_4bit).
+ * Other T / K return QZ_ERR_SHAPE (run the segments one by one). */
+int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T, int K, const void *X, int ldx, int dtype,
+                         int quant_type, int blocksize, int blocksize2, void *stream);
+
 /* Workspace bytes qz_gemm_4bit uses for (T, M, K) at its preferred K split
  * (0 = no split). */
 long long qz_gemm_4bit_workspace_size(int T, int M, int K);

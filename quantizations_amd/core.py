@@ -476,3 +476,56 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
     cd = A.dtype if A.dtype in (torch.float16, torch.bfloat16) else None
     W = dequantize_4bit(B, state, out_dtype=cd).t()
     return torch.nn.functional.linear(A, W.to(A.dtype), None if bias is None else bias.to(A.dtype))
+
+
+# Token counts the multi-token kernel (and so the grouped batched-decode launch) takes
+MT_MIN_TOKENS, MT_MAX_TOKENS, MT_K_MULTIPLE = 2, 16, 256
+
+
+def grouped_tokens_ok(A: Tensor, items) -> bool:
+    """Whether gemm_4bit_grouped can run `items` on A in one launch."""
+    K = A.shape[-1]
+    T = A.numel() // K if K else 0
+    if not (MT_MIN_TOKENS <= T <= MT_MAX_TOKENS and K % MT_K_MULTIPLE == 0
+            and 1 <= len(items) <= _lib.GEMV_MAX_SEGMENTS and A.dtype in (torch.float16, torch.bfloat16)):
+        return False
+    s0 = items[0][1]
+    return all(it[1].shape[1] == K and it[1].quant_type == s0.quant_type and it[1].blocksize == s0.blocksize
+               and it[1].blocksize >= 64 and it[1].nested == s0.nested and it[1].shape[0] % 4 == 0
+               and (not it[1].nested or it[1].state2.blocksize == s0.state2.blocksize) for it in items)
+
+
+def gemm_4bit_grouped(A: Tensor, items) -> list:
+    """Batched decode over a few tokens (2..16) for several 4-bit weights that
+    share A (q/k/v, gate/up of one layer), in ONE launch (qz_gemm_4bit_grouped).
+    items: (B, state, bias[, block_base]) as for gemv_4bit_grouped; returns
+    [y_i] of shape [..., M_i], each bit-identical to gemm_4bit(A, B_i, state_i,
+    bias_i) on the multi-token kernel.  grouped_tokens_ok() says when it applies."""
+    items = list(items)
+    if not grouped_tokens_ok(A, items):
+        raise ValueError("gemm_4bit_grouped needs 2..16 fp16/bf16 tokens, K % 256 == 0, 1..4 weights that share "
+                         "K, quant_type, blocksize (>= 64) and scale format, and out_features % 4 == 0")
+    K = A.shape[-1]
+    lead = A.shape[:-1]
+    A2 = A.reshape(-1, K)
+    if A2.stride(-1) != 1 or A2.stride(0) % 8 != 0 or A2.data_ptr() % 16 != 0:
+        A2 = A2.contiguous()
+    T = A2.shape[0]
+    segs = (_lib.GemvSegment * len(items))()
+    outs = []
+    for i, item in enumerate(items):
+        B, st, bias = item[0], item[1], item[2]
+        block_base = int(item[3]) if len(item) > 3 else 0
+        M = st.shape[0]
+        y = torch.empty((T, M), dtype=A.dtype, device=A.device)
+        if bias is not None and bias.dtype != A.dtype:
+            bias = bias.to(A.dtype)
+        am, qam, am2, code2, off, _ = st.scale_args()
+        segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, block_base, ptr(bias), ptr(y))
+        outs.append(y)
+    s0 = items[0][1]
+    bs2 = int(s0.state2.blocksize) if s0.nested else 0
+    check(lib.qz_gemm_4bit_grouped(len(items), ctypes.cast(segs, ctypes.c_void_p), T, K, ptr(A2), A2.stride(0),
+                                   dtype_code(A.dtype), _lib.QUANT_TYPES[s0.quant_type], s0.blocksize, bs2,
+                                   _lib.stream_of(A)), "gemm_4bit_grouped")
+    return [y.reshape(*lead, y.shape[-1]) for y in outs]

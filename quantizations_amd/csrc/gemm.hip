@@ -61,6 +61,7 @@ struct GemmParams {
   const void *bias;
   void *Y;
   float *ws;          // split-K partials [nsplit][T][M] fp32, or nullptr
+  long long block_base;  // first scale block (row-sharded weights; multi-token kernel only, else 0)
   int T, M, K, ldx, ldy;
   int bs_log2, bs2_log2;
   int k_split;        // K elements per split (multiple of 64)
@@ -224,13 +225,13 @@ __global__ __launch_bounds__(256) void k_gemm_4bit(GemmParams p) {
 // same decode: T tokens cost about one GEMV.
 constexpr int kMtChunk = 256, kMtWaves = 8;
 template <int QT, bool DQ, int DT>
-__global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
+__device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ f4_t s_red[kMtWaves][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * 16;
+  const int m0 = block * 16;
   const int nch = p.K / kMtChunk;
   const int ch0 = wave * nch / kMtWaves, ch1 = (wave + 1) * nch / kMtWaves;
   const int wrow = min(m0 + r, p.M - 1);
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
     st.w[0] = __builtin_nontemporal_load(wp);
     st.w[1] = __builtin_nontemporal_load(wp + 1);
     st.ch = ch;
-    const uint32_t b = (uint32_t)((ebase + ch * kMtChunk) >> p.bs_log2);
+    const uint32_t b = (uint32_t)(p.block_base + ((ebase + ch * kMtChunk) >> p.bs_log2));
     if constexpr (DQ) {
       st.q = p.sc.qabsmax[b];
       st.a = p.sc.absmax2[b >> p.bs2_log2];
@@ -319,6 +320,34 @@ __global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
       store_f32<DT>(p.Y, (long long)c * p.ldy + m, v);
     }
   }
+}
+
+template <int QT, bool DQ, int DT>
+__global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
+  mt_body<QT, DQ, DT>(p, blockIdx.x);
+}
+
+// Grouped multi-token launch: the 2..16-token counterpart of
+// k_gemv_4bit_grouped (q/k/v, gate/up of one layer over a small batch in ONE
+// grid).  Segment i owns workgroups [start[i], start[i+1]); every segment's
+// output is bit-identical to its own k_gemv_4bit_mt launch.
+constexpr int kMtMaxSeg = 4;
+struct GemmGroup {
+  GemmParams seg[kMtMaxSeg];
+  int start[kMtMaxSeg];
+  int nseg;
+};
+
+template <int QT, bool DQ, int DT>
+__global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt_grouped(GemmGroup g) {
+  const int b = blockIdx.x;
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < kMtMaxSeg; ++i)
+    if (i < g.nseg && b >= g.start[i]) s = i;
+  s = __builtin_amdgcn_readfirstlane(s);
+  const GemmParams seg = g.seg[s];
+  mt_body<QT, DQ, DT>(seg, b - g.start[s]);
 }
 
 // Y[t, m] = sum_z ws[z][t][m] (+ bias[m]); 4 consecutive m per thread.
@@ -409,6 +438,7 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
   p.ldy = ldy;
   p.bs_log2 = bsl;
   p.bs2_log2 = bs2l;
+  p.block_base = 0;
   int bt, nsplit;
   hipStream_t s = (hipStream_t)stream;
   if (mt_ok(T, K)) {  // 2..16 tokens: multi-token MFMA GEMV, one launch
@@ -454,5 +484,62 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
       hipLaunchKernelGGL((k_gemm_reduce<QZ_DT_BF16>), dim3(g), dim3(256), 0, s, workspace, nsplit, T, M, bias, Y, ldy);
     QZ_LAUNCH_CHECK();
   }
+  return QZ_OK;
+}
+
+extern "C" int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T, int K, const void *X, int ldx,
+                                    int dtype, int quant_type, int blocksize, int blocksize2, void *stream) {
+  if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs || !X || T < 0 || K < 0) return QZ_ERR_ARG;
+  if (quant_type != QZ_FP4 && quant_type != QZ_NF4) return QZ_ERR_DTYPE;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_DTYPE;
+  const bool dq = segs[0].qabsmax != nullptr;
+  const int bsl = ilog2g(blocksize), bs2l = dq ? ilog2g(blocksize2) : 0;
+  if (bsl < 6 || bs2l < 0) return QZ_ERR_BLOCKSIZE;
+  if (!mt_ok(T, K) || ldx < K || (ldx % 8) != 0 || (reinterpret_cast<uintptr_t>(X) % 16) != 0) return QZ_ERR_SHAPE;
+  GemmGroup g;
+  g.nseg = nseg;
+  int blocks = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const qz_gemv_segment &q = segs[i];
+    if (!q.B || !q.y || q.M < 0) return QZ_ERR_ARG;
+    if ((q.absmax == nullptr) == (q.qabsmax == nullptr) || (q.qabsmax != nullptr) != dq) return QZ_ERR_ARG;
+    if (dq && (!q.absmax2 || !q.code2 || !q.offset)) return QZ_ERR_ARG;
+    if ((q.M % 4) != 0 || (reinterpret_cast<uintptr_t>(q.B) % 16) != 0 || q.block_base < 0 ||
+        q.block_base + (long long)q.M * K / blocksize >= (1LL << 32))
+      return QZ_ERR_SHAPE;
+    GemmParams &p = g.seg[i];
+    p.X = X;
+    p.B = q.B;
+    p.sc = ScaleSrc{q.absmax, q.qabsmax, q.absmax2, q.code2, q.offset, blocksize2};
+    p.bias = q.bias;
+    p.Y = q.y;
+    p.ws = nullptr;
+    p.block_base = q.block_base;
+    p.T = T;
+    p.M = q.M;
+    p.K = K;
+    p.ldx = ldx;
+    p.ldy = q.M;
+    p.bs_log2 = bsl;
+    p.bs2_log2 = bs2l;
+    p.k_split = K;
+    g.start[i] = blocks;
+    blocks += (q.M + 15) / 16;
+  }
+  for (int i = nseg; i < kMtMaxSeg; ++i) g.start[i] = blocks;
+  if (blocks == 0 || T == 0) return QZ_OK;
+  hipStream_t s = (hipStream_t)stream;
+#define QZ_MTG(QT_, DQ_, DT_) \
+  hipLaunchKernelGGL((k_gemv_4bit_mt_grouped<QT_, DQ_, DT_>), dim3(blocks), dim3(64 * kMtWaves), 0, s, g)
+#define QZ_MTG_DT(QT_, DQ_) \
+  do { if (dtype == QZ_DT_F16) QZ_MTG(QT_, DQ_, QZ_DT_F16); else QZ_MTG(QT_, DQ_, QZ_DT_BF16); } while (0)
+  if (quant_type == QZ_FP4) {
+    if (dq) QZ_MTG_DT(QZ_FP4, true); else QZ_MTG_DT(QZ_FP4, false);
+  } else {
+    if (dq) QZ_MTG_DT(QZ_NF4, true); else QZ_MTG_DT(QZ_NF4, false);
+  }
+#undef QZ_MTG_DT
+#undef QZ_MTG
+  QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

@@ -14,7 +14,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .core import Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemv_4bit, gemv_4bit_grouped
+from .core import (MT_MAX_TOKENS, Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemm_4bit_grouped, gemv_4bit,
+                   gemv_4bit_grouped, grouped_tokens_ok)
 
 
 def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None):
@@ -28,12 +29,14 @@ def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: 
 
 class DecodeGroup:
     """Linear4bit layers that read the same input (q/k/v or gate/up of one
-    decoder layer), fused for batch-1 decode into one grouped GEMV launch
-    (SURVEY.md 8f row 2).  The first member called with a decode-shaped x
-    computes every member's output; the others pick theirs up if they are
-    called with the SAME tensor object (identity + version check, so a new or
-    modified input always recomputes).  Prefill inputs bypass the group.
-    Built by ``integration.fuse_projection_groups``."""
+    decoder layer), fused for decode into one grouped launch (SURVEY.md 8f
+    row 2): one grouped GEMV for a single token, one grouped multi-token GEMM
+    for a small batch of decode streams (2..16 tokens).  The first member
+    called with a decode-shaped x computes every member's output; the others
+    pick theirs up if they are called with the SAME tensor object (identity +
+    version check, so a new or modified input always recomputes).  Prefill
+    inputs (more tokens) bypass the group.  Built by
+    ``integration.fuse_projection_groups``."""
 
     def __init__(self, members, compute):
         self.members = list(members)
@@ -41,6 +44,12 @@ class DecodeGroup:
         self._x = None                   # weakref to the input the cached outputs belong to
         self._ver = -1
         self._outs = {}
+
+    @staticmethod
+    def accepts(x: torch.Tensor) -> bool:
+        """Decode-shaped input: 1..MT_MAX_TOKENS tokens."""
+        k = x.shape[-1]
+        return k > 0 and 1 <= x.numel() // k <= MT_MAX_TOKENS
 
     @staticmethod
     def _version(x: torch.Tensor) -> int:
@@ -69,7 +78,12 @@ def _linear4bit_group_compute(group: DecodeGroup, x: torch.Tensor):
     for m in group.members:
         bias = None if m.bias is None else m.bias.to(xin.dtype)
         items.append((m.weight, m.weight.quant_state, bias))
-    outs = gemv_4bit_grouped(xin, items)
+    if xin.numel() == xin.shape[-1]:
+        outs = gemv_4bit_grouped(xin, items)
+    elif grouped_tokens_ok(xin, items):
+        outs = gemm_4bit_grouped(xin, items)
+    else:  # shapes the multi-token kernel does not take: each member as it would run alone
+        outs = [matmul_4bit(xin, w, bias=b, quant_state=st) for w, st, b in items]
     return [o if o.dtype == inp_dtype else o.to(inp_dtype) for o in outs]
 
 
@@ -111,7 +125,7 @@ class Linear4bit(nn.Linear):
         if qs is None:
             raise RuntimeError("Linear4bit weight is not quantised yet: move the module to a GPU first")
         group = self.__dict__.get("_qz_group")
-        if group is not None and x.numel() == x.shape[-1]:
+        if group is not None and group.accepts(x):
             return group.take(self, x)
         inp_dtype = x.dtype
         xin = self._input(x)

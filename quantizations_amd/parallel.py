@@ -106,7 +106,7 @@ class RowShardedLinear4bit(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         group = self.__dict__.get("_qz_group")
-        if group is not None and x.numel() == x.shape[-1]:
+        if group is not None and group.accepts(x):
             return group.take(self, x)
         y = self.local_forward(x)                       # [..., M/P]
         if not self.gather:
@@ -123,14 +123,49 @@ class RowShardedLinear4bit(nn.Module):
         return full.reshape(*lead, self.world_size * rows)
 
 
+def _sharded_group_tokens(group, x: torch.Tensor):
+    """T = 2..16 decode tokens (a small batch of streams): ONE grouped
+    multi-token launch for the members' row shards, then (gather mode) ONE
+    all-gather of the [T, sum(rows)] concatenation."""
+    from .core import gemm_4bit_grouped, grouped_tokens_ok
+
+    ms = group.members
+    K = x.shape[-1]
+    T = x.numel() // K
+    lead = x.shape[:-1]
+    items = [(m.packed, m.state, m.bias, m.block_base) for m in ms]
+    if ms[0]._local_matmul is not None:  # test hook (CPU)
+        outs = [m._local_matmul(x, m) for m in ms]
+    elif grouped_tokens_ok(x, items):
+        outs = gemm_4bit_grouped(x, items)
+    else:
+        outs = [m.local_forward(x) for m in ms]
+    if not ms[0].gather:  # column-parallel: each member keeps its shard
+        return [o.reshape(*lead, o.shape[-1]) for o in outs]
+    rows = [m.r1 - m.r0 for m in ms]
+    S = sum(rows)
+    P = ms[0].world_size
+    buf = torch.cat([o.reshape(T, r) for o, r in zip(outs, rows)], dim=1).contiguous()   # [T, S]
+    gathered = torch.empty((P * T, S), dtype=buf.dtype, device=buf.device)
+    dist.all_gather_into_tensor(gathered, buf, group=ms[0].group)
+    gathered = gathered.view(P, T, S)
+    res, o = [], 0
+    for r in rows:
+        res.append(gathered[:, :, o:o + r].permute(1, 0, 2).reshape(*lead, P * r))
+        o += r
+    return res
+
+
 def sharded_group_compute(group, x: torch.Tensor):
     """Decode step of a DecodeGroup of RowShardedLinear4bit layers: ONE grouped
     local GEMV writes every member's row shard into one buffer, ONE all-gather
     exchanges it (instead of one all-gather per layer: bs=1 decode collectives
     are latency-bound), then each member's full output is cut out of the
-    [world, sum(rows)] result."""
+    [world, sum(rows)] result.  2..16 tokens: _sharded_group_tokens."""
     from .core import gemv_4bit_grouped
 
+    if x.numel() != x.shape[-1]:
+        return _sharded_group_tokens(group, x)
     ms = group.members
     rows = [m.r1 - m.r0 for m in ms]
     S = sum(rows)

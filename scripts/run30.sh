@@ -1,0 +1,15 @@
+# grouped multi-token decode: GPU parity suite, batched decode benches (1 GPU; RCCL world 1)
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -4 "gpurun_out/$name.log"
+  [ $rc -eq 0 ] || exit $rc
+}
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step bench_b4 300 python bench.py --steps 16 --warmup 4 --no-prefill --no-cpu --no-roofline --batch 4
+step bench_b8 300 python bench.py --steps 16 --warmup 4 --no-prefill --no-cpu --no-roofline --batch 8
+step bench_shard_b4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --force-shard --batch 4 --steps 16 --warmup 4 --no-roofline --no-prefill --no-cpu

@@ -143,12 +143,16 @@ def _group_worker(rank, world, port, q):
                        + b.float().numpy()).astype(np.float16)
                 ok = ok and tuple(y.shape) == (1, 1, st.packed.size * 2 // 512) and \
                     bool(np.array_equal(y.reshape(-1).numpy(), ref))
-        # prefill (T > 1) bypasses the group and keeps the fp32 hook output
-        xp = torch.randn(1, 3, 512, generator=g).to(torch.float16)
-        yp = parent.k_proj(xp)
-        st, b = refs["k_proj"]
-        refp = np.stack([oracle.gemv(r, st) for r in xp.reshape(3, 512).float().numpy()]).astype(np.float32)
-        ok = ok and bool(np.array_equal(yp.reshape(3, -1).numpy(), refp + b.float().numpy()))
+        # a small batch of decode tokens (3) runs through the group with ONE all-gather of
+        # [T, sum(rows)]; a 20-token prefill bypasses it -- both keep the fp32 hook output
+        for T in (3, 20):
+            xp = torch.randn(1, T, 512, generator=g).to(torch.float16)
+            for name in ("q_proj", "k_proj", "v_proj"):
+                yp = getattr(parent, name)(xp)
+                st, b = refs[name]
+                refp = np.stack([oracle.gemv(r, st) for r in xp.reshape(T, 512).float().numpy()]).astype(np.float32)
+                ok = ok and tuple(yp.shape) == (1, T, st.packed.size * 2 // 512) and \
+                    bool(np.array_equal(yp.reshape(T, -1).numpy(), refp + b.float().numpy()))
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()

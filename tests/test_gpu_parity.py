@@ -454,6 +454,81 @@ def test_gemv_grouped_row_shards(orc):
         assert_close(y.float().cpu(), f[:, sh.r0:sh.r1].float().cpu().numpy(), torch.float16, "grouped shard")
 
 
+@pytest.mark.parametrize("T", [2, 5, 16])
+@pytest.mark.parametrize("qt,dq,dtype", [("nf4", True, torch.float16), ("fp4", False, torch.float16),
+                                         ("nf4", True, torch.bfloat16)])
+def test_gemm_grouped_multitoken_bit_identical(T, qt, dq, dtype):
+    """Grouped multi-token launch (q/k/v-style segments over a small batch of
+    decode tokens) == each segment's own gemm_4bit (the multi-token kernel),
+    bit for bit; row shards with block_base != 0 == the full weight's rows."""
+    from quantizations_amd.core import gemm_4bit, gemm_4bit_grouped, grouped_tokens_ok, quantize_4bit
+    from quantizations_amd.parallel import shard_rows
+
+    K = 1024
+    x = torch.randn(T, K, generator=torch.Generator().manual_seed(T), dtype=torch.float32).to(dtype).to(DEV)
+    items, singles = [], []
+    for i, M in enumerate((512, 128, 96)):
+        packed, st = quantize_4bit(_w(M, K, seed=200 + i).to(DEV), quant_type=qt, compress_statistics=dq)
+        bias = torch.randn(M, generator=torch.Generator().manual_seed(i)).to(dtype).to(DEV) if i == 2 else None
+        items.append((packed, st, bias))
+        singles.append(gemm_4bit(x, packed, st, bias=bias, route="fused"))
+    assert grouped_tokens_ok(x, items)
+    ys = gemm_4bit_grouped(x, items)
+    for y, r in zip(ys, singles):
+        assert y.shape == r.shape and y.dtype == dtype
+        assert torch.equal(y, r)
+    # row shards of a double-quant weight whose second shard starts inside a 256-block group
+    packed, st = quantize_4bit(_w(72, K, seed=300).to(DEV), quant_type=qt, compress_statistics=dq)  # 36-row shards
+    full = gemm_4bit(x, packed, st, route="fused")
+    shards = [shard_rows(packed, st, r, 2) for r in range(2)]
+    ys = gemm_4bit_grouped(x, [(sh.packed, sh.state, None, sh.block_base) for sh in shards])
+    if dq:
+        assert shards[1].block_base != 0
+    for y, sh in zip(ys, shards):
+        assert torch.equal(y, full[:, sh.r0:sh.r1])
+
+
+def test_gemm_grouped_rejects_unsupported():
+    from quantizations_amd.core import gemm_4bit_grouped, grouped_tokens_ok, quantize_4bit
+
+    a = quantize_4bit(_w(64, 512).to(DEV), quant_type="nf4")
+    x1 = torch.randn(1, 512, device=DEV, dtype=torch.float16)
+    x20 = torch.randn(20, 512, device=DEV, dtype=torch.float16)
+    x_k = torch.randn(3, 320, device=DEV, dtype=torch.float16)
+    b = quantize_4bit(_w(64, 320).to(DEV), quant_type="nf4")
+    assert not grouped_tokens_ok(x1, [(a[0], a[1], None)])      # one token: the grouped GEMV's job
+    assert not grouped_tokens_ok(x20, [(a[0], a[1], None)])     # > 16 tokens: prefill
+    assert not grouped_tokens_ok(x_k, [(b[0], b[1], None)])     # K % 256 != 0
+    with pytest.raises(ValueError):
+        gemm_4bit_grouped(x20, [(a[0], a[1], None)])
+
+
+def test_tiny_llama_batched_decode_groups():
+    """Three bs=1 decode streams in one batch (the bench's weak-scaling layout
+    per GPU): with fuse_projection_groups the q/k/v and gate/up members run as
+    one grouped multi-token launch each and the logits equal the unfused
+    model's bit for bit; a 20-token prefill bypasses the groups."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import fuse_projection_groups, replace_with_bnb_linear
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=512)
+    torch.manual_seed(4)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, quant_type="nf4")
+    ids = torch.randint(0, 512, (3, 20), device=DEV)
+    with torch.no_grad():
+        ref = model(input_ids=ids, use_cache=True)
+        tok = ref.logits[:, -1:].argmax(-1)
+        ref_step = model(input_ids=tok, past_key_values=ref.past_key_values, use_cache=True).logits
+        assert fuse_projection_groups(model) == 2 * cfg.num_hidden_layers
+        out = model(input_ids=ids, use_cache=True)
+        assert torch.equal(out.logits, ref.logits)
+        step = model(input_ids=tok, past_key_values=out.past_key_values, use_cache=True).logits
+    assert torch.equal(step, ref_step)
+
+
 # ---------------------------------------------------------------------------
 # fused prefill GEMM (MFMA)
 # ---------------------------------------------------------------------------

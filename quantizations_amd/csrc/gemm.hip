@@ -220,14 +220,25 @@ __global__ __launch_bounds__(256) void k_gemm_4bit(GemmParams p) {
 // 64g .. 64g+63 -- one whole scale block, and with its 3 neighbours a full
 // 128-B line of the row -- builds that block's exact 16-bit table and decodes
 // its 8 dwords into the A fragments of 8 v_mfma_f32_16x16x32 (A = weights, M
-// dimension; B = the T tokens, N dimension, zero-padded to 16, loaded by lane
-// (c = l % 16, g) from L2 in the same pair order).  Every token rides on the
-// same decode: T tokens cost about one GEMV.
+// dimension; B = the T tokens, N dimension, zero-padded to 16).  Every token
+// rides on the same decode: T tokens cost about one GEMV.
+//
+// The B fragments (lane (c, g) of MFMA j needs x[c][64g + 8j .. +8]) touch 64
+// different lines per wave instruction when loaded straight from memory.
+// TB > 0 (production): the wave instead stages its chunk of X -- TB token
+// rows x 512 B, loaded with plain coalesced 16-B loads (two token rows per
+// wave instruction) together with the weights -- into a wave-private LDS
+// image in the decode's pair order, and reads the fragments from there
+// (ds_read_b128, rows padded to 528 B: conflict-free); lanes c >= T read a
+// zero row.  TB = 0: the direct fragment loads (kept for the microbenchmark).
 constexpr int kMtChunk = 256, kMtWaves = 8;
-template <int QT, bool DQ, int DT>
+constexpr int kMtXRow = kMtChunk * 2 + 16;  // padded LDS row of one token's chunk of X
+template <int QT, bool DQ, int DT, int TB = 0>
 __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
+  constexpr int XL = TB > 0 ? (TB + 1) / 2 : 1;  // staging loads per lane per chunk (two token rows each)
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ f4_t s_red[kMtWaves][64];
+  __shared__ __attribute__((aligned(16))) unsigned char s_xs[TB > 0 ? kMtWaves * (TB + 1) * kMtXRow : 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -240,12 +251,17 @@ __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
   const long long ebase = (long long)wrow * p.K + 64 * g;
   const bool tok = r < p.T;  // as a B-operand lane, lane l carries token c = l % 16
   const uint16_t *xrow = reinterpret_cast<const uint16_t *>(p.X) + (size_t)min(r, p.T - 1) * p.ldx + 64 * g;
+  // TB > 0: staging lane map -- load i covers token rows 2i, 2i+1; lane l -> row 2i + l/32, 16-B piece l % 32
+  unsigned char *xs = s_xs + (TB > 0 ? wave * (TB + 1) * kMtXRow : 0);
+  const int spc = lane & 31, shalf = lane >> 5;
+  const uint16_t *xstage = reinterpret_cast<const uint16_t *>(p.X) + 8 * spc;
+  // fragment reads: token row c (< T) or the zero row TB
+  const uint32_t frag_off = (uint32_t)((tok ? r : TB) * kMtXRow + g * 128);
 
   // two NAMED stages (a dynamically indexed register array would live in scratch)
-  // (the token fragments are loaded at consume time: each B-fragment load touches
-  // 64 lines, and keeping two sets in flight measured slower at T = 16)
   struct Stage {
     v4u w[2];
+    v4u x[XL];
     uint32_t q;
     float a;
     int ch;
@@ -263,13 +279,34 @@ __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
       st.q = 0u;
       st.a = p.sc.absmax[b];
     }
+    if constexpr (TB > 0) {
+#pragma unroll
+      for (int i = 0; i < XL; ++i) {  // rows >= T re-read row T-1 (never stored to LDS)
+        const int t = min(2 * i + shalf, p.T - 1);
+        st.x[i] = *reinterpret_cast<const v4u *>(xstage + (size_t)t * p.ldx + ch * kMtChunk);
+      }
+    }
   };
   f4_t acc = f4_t{0.f, 0.f, 0.f, 0.f};
   float offset = 0.0f;
   auto consume = [&](const Stage &st) {
-    v4u x[8];
+    v4u bfr[8];
+    if constexpr (TB > 0) {
+      // stage this chunk's X rows (pair order) into the wave's image, then read the fragments
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = *reinterpret_cast<const v4u *>(xrow + st.ch * kMtChunk + 8 * j);
+      for (int i = 0; i < XL; ++i) {
+        const int t = 2 * i + shalf;
+        if (t < p.T) *reinterpret_cast<v4u *>(xs + t * kMtXRow + spc * 16) = pair_order(st.x[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bfr[j] = *reinterpret_cast<const v4u *>(xs + frag_off + j * 16);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const v4u xv = *reinterpret_cast<const v4u *>(xrow + st.ch * kMtChunk + 8 * j);
+        bfr[j] = tok ? pair_order(xv) : v4u{0u, 0u, 0u, 0u};
+      }
+    }
     float am;
     if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[st.q], st.a), offset);
     else am = st.a;
@@ -281,17 +318,19 @@ __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
       uint32_t P[4];
       decode_codes(w[j], t, P);
       const v4u af = v4u{P[0], P[1], P[2], P[3]};
-      const v4u bf = tok ? pair_order(x[j]) : v4u{0u, 0u, 0u, 0u};
       if constexpr (DT == QZ_DT_F16)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, af), __builtin_bit_cast(h8_t, bf), acc,
-                                                     0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, af), __builtin_bit_cast(h8_t, bfr[j]),
+                                                     acc, 0, 0, 0);
       else
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, af), __builtin_bit_cast(b8_t, bf),
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, af), __builtin_bit_cast(b8_t, bfr[j]),
                                                       acc, 0, 0, 0);
     }
   };
   Stage s0, s1;
   if (ch0 < ch1) load(s0, ch0);  // first HBM requests go out before anything else
+  if constexpr (TB > 0) {  // the wave's zero row (B columns of absent tokens)
+    for (int i = lane; i < kMtXRow / 4; i += 64) reinterpret_cast<uint32_t *>(xs + TB * kMtXRow)[i] = 0u;
+  }
   if constexpr (DQ) {
     if (tid < 256) s_code2[tid] = p.sc.code2[tid];
     offset = *p.sc.offset;
@@ -322,10 +361,13 @@ __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
   }
 }
 
-template <int QT, bool DQ, int DT>
+template <int QT, bool DQ, int DT, int TB>
 __global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
-  mt_body<QT, DQ, DT>(p, blockIdx.x);
+  mt_body<QT, DQ, DT, TB>(p, blockIdx.x);
 }
+
+// token bucket of the staged multi-token kernel: LDS image rows per wave
+static int mt_bucket(int T) { return T <= 2 ? 2 : T <= 4 ? 4 : T <= 8 ? 8 : 16; }
 
 // Grouped multi-token launch: the 2..16-token counterpart of
 // k_gemv_4bit_grouped (q/k/v, gate/up of one layer over a small batch in ONE
@@ -338,7 +380,7 @@ struct GemmGroup {
   int nseg;
 };
 
-template <int QT, bool DQ, int DT>
+template <int QT, bool DQ, int DT, int TB>
 __global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt_grouped(GemmGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -347,7 +389,7 @@ __global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt_grouped(GemmGrou
     if (i < g.nseg && b >= g.start[i]) s = i;
   s = __builtin_amdgcn_readfirstlane(s);
   const GemmParams seg = g.seg[s];
-  mt_body<QT, DQ, DT>(seg, b - g.start[s]);
+  mt_body<QT, DQ, DT, TB>(seg, b - g.start[s]);
 }
 
 // Y[t, m] = sum_z ws[z][t][m] (+ bias[m]); 4 consecutive m per thread.
@@ -445,7 +487,16 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
     p.ws = nullptr;
     p.k_split = K;
     const dim3 grid((unsigned)((M + 15) / 16));
-#define QZ_MT(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemv_4bit_mt<QT_, DQ_, DT_>), grid, dim3(64 * kMtWaves), 0, s, p)
+    const int tb = mt_bucket(T);
+#define QZ_MTB(QT_, DQ_, DT_, TB_) \
+  hipLaunchKernelGGL((k_gemv_4bit_mt<QT_, DQ_, DT_, TB_>), grid, dim3(64 * kMtWaves), 0, s, p)
+#define QZ_MT(QT_, DQ_, DT_)                                             \
+  do {                                                                   \
+    if (tb == 2) QZ_MTB(QT_, DQ_, DT_, 2);                               \
+    else if (tb == 4) QZ_MTB(QT_, DQ_, DT_, 4);                          \
+    else if (tb == 8) QZ_MTB(QT_, DQ_, DT_, 8);                          \
+    else QZ_MTB(QT_, DQ_, DT_, 16);                                      \
+  } while (0)
 #define QZ_MT_DT(QT_, DQ_) \
   do { if (dtype == QZ_DT_F16) QZ_MT(QT_, DQ_, QZ_DT_F16); else QZ_MT(QT_, DQ_, QZ_DT_BF16); } while (0)
     if (quant_type == QZ_FP4) {
@@ -455,6 +506,7 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
     }
 #undef QZ_MT_DT
 #undef QZ_MT
+#undef QZ_MTB
     QZ_LAUNCH_CHECK();
     return QZ_OK;
   }
@@ -529,8 +581,16 @@ extern "C" int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T
   for (int i = nseg; i < kMtMaxSeg; ++i) g.start[i] = blocks;
   if (blocks == 0 || T == 0) return QZ_OK;
   hipStream_t s = (hipStream_t)stream;
-#define QZ_MTG(QT_, DQ_, DT_) \
-  hipLaunchKernelGGL((k_gemv_4bit_mt_grouped<QT_, DQ_, DT_>), dim3(blocks), dim3(64 * kMtWaves), 0, s, g)
+  const int tb = mt_bucket(T);
+#define QZ_MTGB(QT_, DQ_, DT_, TB_) \
+  hipLaunchKernelGGL((k_gemv_4bit_mt_grouped<QT_, DQ_, DT_, TB_>), dim3(blocks), dim3(64 * kMtWaves), 0, s, g)
+#define QZ_MTG(QT_, DQ_, DT_)                                            \
+  do {                                                                   \
+    if (tb == 2) QZ_MTGB(QT_, DQ_, DT_, 2);                              \
+    else if (tb == 4) QZ_MTGB(QT_, DQ_, DT_, 4);                         \
+    else if (tb == 8) QZ_MTGB(QT_, DQ_, DT_, 8);                         \
+    else QZ_MTGB(QT_, DQ_, DT_, 16);                                     \
+  } while (0)
 #define QZ_MTG_DT(QT_, DQ_) \
   do { if (dtype == QZ_DT_F16) QZ_MTG(QT_, DQ_, QZ_DT_F16); else QZ_MTG(QT_, DQ_, QZ_DT_BF16); } while (0)
   if (quant_type == QZ_FP4) {
@@ -540,6 +600,7 @@ extern "C" int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T
   }
 #undef QZ_MTG_DT
 #undef QZ_MTG
+#undef QZ_MTGB
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

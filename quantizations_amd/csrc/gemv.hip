@@ -853,7 +853,7 @@ static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_
 using namespace qz;
 
 // Geometry (WK = waves along K, R = rows per wave) for the byte-table decode,
-// from the measured shape sweep in DESIGN.md section 4.1 (scripts/run24.sh):
+// from the measured shape sweep in DESIGN.md section 4.1 (scripts/gpu_sessions/run24.sh):
 //  * >= 64 Mi weights (gate/up groups, 8192x28672, ...): R=4 -- more bytes in
 //    flight per wave and fewer x/scale loads per weight byte;
 //  * smaller: R=2;

@@ -213,6 +213,210 @@ __global__ __launch_bounds__(256) void k_gemm_4bit(GemmParams p) {
   }
 }
 
+// Large-T prefill: 256 x 256 output tile (256 tokens x 256 weight rows), 8
+// waves as 2 (tokens) x 4 (rows), each wave 128 tokens x 64 rows = 4 x 8
+// v_mfma_f32_16x16x32 accumulators, K-step 64 (one scale block per row).
+//   * X (the B operand) goes global -> LDS with global_load_lds_dwordx4 (no
+//     VGPRs, no VALU): the LDS image is lane-linear per wave instruction, so the
+//     16-B-chunk XOR swizzle of lds_off() is applied to the per-lane SOURCE
+//     address (the read applies the same involution).
+//   * W (the A operand) is register-staged: a thread owns 32 codes of one
+//     (row, block); its packed bytes and scale for step s+1 are loaded while
+//     step s multiplies, then decoded -- through the exact per-block table, in
+//     natural element order to match X -- into the other LDS buffer.  The W
+//     operand is bit-identical to dequantize_4bit's.
+//   * One barrier per K-step (its vmcnt(0) retires the next step's X DMA and W loads).
+//   * Epilogue through LDS: accumulators (+ bias) -> fp16/bf16 rows of 128 B
+//     per wave, then 16-B coalesced stores of Y rows.
+//   * XCD-aware tile order: each XCD walks a contiguous range of tiles (token
+//     tile major), so the tiles in flight on one XCD share X/W k-slices in its L2.
+constexpr int kBigT = 256, kBigM = 256;
+constexpr int kBigStage = kBigT * 128;              // one buffer of X or W: 256 rows x 64 elements x 2 B
+constexpr int kBigLds = 4 * kBigStage;              // X[2] + W[2] = 128 KiB
+constexpr int kBigERow = 144;                       // epilogue image row: 64 outputs x 2 B + 16 B pad
+constexpr int kBigMinT = 4096;  // below this the 128-row tile kernel (with split-K) is faster (gemm_micro)
+
+// V (schedule variant, microbenchmark A/B): 0 = decode after the step's MFMAs with a
+// scheduling fence per fragment half; 1 = no fences; 2 = decode between the two k-halves.
+template <int QT, bool DQ, int DT, int V = 0>
+__global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kBigLds + (DQ ? 1024 : 0)];
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  typedef __attribute__((address_space(1))) void *glb_ptr_t;
+  float *s_code2 = reinterpret_cast<float *>(smem + kBigLds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 2, wm = wave & 3;
+
+  // XCD-aware, bijective tile order (blocks are dealt to the 8 XCDs round-robin)
+  const int tiles_m = (p.M + kBigM - 1) / kBigM;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (wg % tiles_m) * kBigM, t0 = (wg / tiles_m) * kBigT;
+  const int nsteps = p.K / kBK;
+
+  // X staging: instruction i of wave w fills LDS rows 8*(8i + w) .. +8 (1 KiB, lane-linear);
+  // lane l lands in row 8*(8i+w) + l/8, 16-B slot l%8, which holds chunk slot ^ ((row >> 1) & 7)
+  // (32-bit byte offsets from the uniform X base: the host guarantees T * ldx * 2 < 2^32)
+  const unsigned char *xbase = reinterpret_cast<const unsigned char *>(p.X);
+  uint32_t xoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (8 * i + wave) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    xoff[i] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * chunk) * 2u;
+  }
+  auto stage_x = [&](int step, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(xbase + xoff[i] + (uint32_t)step * (kBK * 2)),
+                                       (lds_ptr_t)(smem + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
+  };
+
+  // W staging: thread -> (row wr, 32-code half wh of the 64-code step)
+  const int wr = tid >> 1, wh = tid & 1;
+  const int wrow = min(m0 + wr, p.M - 1);  // clamped rows are computed and never stored
+  const unsigned char *wptr = p.B + (size_t)wrow * ((uint32_t)p.K >> 1) + 16 * wh;
+  const uint32_t blk_row = (uint32_t)(((long long)wrow * p.K) >> p.bs_log2);
+  struct WStage {
+    v4u w;
+    uint32_t q;
+    float a;
+  };
+  auto load_w = [&](WStage &st, int step) {
+    const int k0 = step * kBK;
+    st.w = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(wptr + (k0 >> 1)));
+    const uint32_t b = blk_row + ((uint32_t)k0 >> p.bs_log2);
+    if constexpr (DQ) {
+      st.q = p.sc.qabsmax[b];
+      st.a = p.sc.absmax2[b >> p.bs2_log2];
+    } else {
+      st.q = 0u;
+      st.a = p.sc.absmax[b];
+    }
+  };
+  float offset = 0.0f;
+  auto store_w = [&](const WStage &st, int buf) {
+    float am;
+    if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[st.q], st.a), offset);  // core.py:467-468
+    else am = st.a;
+    uint32_t t[8];
+    block_table<QT, DT>(am, t);
+    const uint32_t w[4] = {st.w.x, st.w.y, st.w.z, st.w.w};
+    unsigned char *sw = smem + (2 + buf) * kBigStage;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t N[4];
+      decode_codes_natural(w[d], t, N);
+      *reinterpret_cast<v4u *>(sw + lds_off(wr, 4 * wh + d)) = v4u{N[0], N[1], N[2], N[3]};
+    }
+  };
+
+  f4_t acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+  // Fragment addresses: every fragment row is 16 * n + fr, so the chunk swizzle ((row >> 1) & 7)
+  // is (fr >> 1) & 7 for all of them and chunk 4 * kk + fk lands at slot (fk ^ swz) ^ 4 * kk:
+  // one lane offset per kk, everything else a compile-time / wave-uniform offset (no per-fragment
+  // address registers live across the K loop).
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t frag_lane[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                                 (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  auto mfma_half = [&](int buf, int kk) {
+    const unsigned char *sx = smem + buf * kBigStage + (128 * wt) * 128;
+    const unsigned char *sw = smem + (2 + buf) * kBigStage + (64 * wm) * 128;
+    {
+      v4u aw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) aw[j] = *reinterpret_cast<const v4u *>(sw + frag_lane[kk] + 16 * j * 128);
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {  // token fragments in two halves: 16 fewer live VGPRs
+        v4u bx[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          bx[i] = *reinterpret_cast<const v4u *>(sx + frag_lane[kk] + 16 * (4 * ih + i) * 128);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            f4_t &c = acc[j][4 * ih + i];
+            if constexpr (DT == QZ_DT_F16)
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, aw[j]), __builtin_bit_cast(h8_t, bx[i]),
+                                                         c, 0, 0, 0);
+            else
+              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, aw[j]),
+                                                          __builtin_bit_cast(b8_t, bx[i]), c, 0, 0, 0);
+          }
+        if constexpr (V == 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  // W is prefetched one step ahead into ONE register set: step s issues W(s+1)'s loads right
+  // after X(s+1)'s DMA, multiplies buffer s & 1, then decodes W(s+1) into the other buffer.
+  // (A two-set ring needs the loop unrolled by two; its extra live registers spilled the
+  // accumulators.)
+  WStage ws;
+  stage_x(0, 0);
+  load_w(ws, 0);
+  if constexpr (DQ) {
+    if (tid < 256) s_code2[tid] = p.sc.code2[tid];
+    offset = *p.sc.offset;
+  }
+  __syncthreads();
+  store_w(ws, 0);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      stage_x(s + 1, cur ^ 1);
+      load_w(ws, s + 1);
+    }
+    mfma_half(cur, 0);
+    if (V == 2 && more) store_w(ws, cur ^ 1);
+    mfma_half(cur, 1);
+    if (more) {
+      if (V != 2) store_w(ws, cur ^ 1);
+      __syncthreads();  // X(s+1) DMA + W(s+1) decode visible to every wave; buffer cur free
+    }
+  }
+
+  // ---- epilogue: lane holds weight rows 16j + 4*fk + r (r = 0..3) of token 16i + fr ----
+  __syncthreads();  // every wave is done with the staging buffers
+  unsigned char *ew = smem + wave * (64 * kBigERow);
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = min(m0 + 64 * wm + 16 * j + 4 * fk + r, p.M - 1);
+      bv[j][r] = p.bias ? load_f32<DT>(p.bias, m) : 0.0f;
+    }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4_t v = acc[j][4 * h + i];
+        const uint32_t lo = cvt_pk16<DT>(v[0] + bv[j][0], v[1] + bv[j][1]);
+        const uint32_t hi = cvt_pk16<DT>(v[2] + bv[j][2], v[3] + bv[j][3]);
+        *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * kBigERow + (16 * j + 4 * fk) * 2) = uint2{lo, hi};
+      }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int qd = lane + 64 * it, tok = qd >> 3, c16 = qd & 7;
+      const v4u v = *reinterpret_cast<const v4u *>(ew + tok * kBigERow + c16 * 16);
+      const int t = t0 + 128 * wt + 64 * h + tok, m = m0 + 64 * wm + 8 * c16;
+      if (t < p.T && m < p.M)
+        *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
+    }
+  }
+}
+
 // Multi-token GEMV for 2 <= T <= 16 (small-batch decode, short prefills).
 // A 512-thread workgroup owns 16 weight rows; its 8 waves split K and meet in
 // LDS (no workspace, no second launch).  Per 256-element chunk, lane
@@ -507,6 +711,24 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
 #undef QZ_MT_DT
 #undef QZ_MT
 #undef QZ_MTB
+    QZ_LAUNCH_CHECK();
+    return QZ_OK;
+  }
+  if (T >= kBigMinT && (M % 8) == 0 && (ldy % 8) == 0 && (reinterpret_cast<uintptr_t>(Y) % 16) == 0 &&
+      (long long)T * ldx * 2 < (1LL << 32)) {  // large T: the 256 x 256 tile kernel
+    p.ws = nullptr;
+    p.k_split = K;
+    const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
+#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_big<QT_, DQ_, DT_>), dim3(g), dim3(512), 0, s, p)
+#define QZ_BIG_DT(QT_, DQ_) \
+  do { if (dtype == QZ_DT_F16) QZ_BIG(QT_, DQ_, QZ_DT_F16); else QZ_BIG(QT_, DQ_, QZ_DT_BF16); } while (0)
+    if (quant_type == QZ_FP4) {
+      if (dq) QZ_BIG_DT(QZ_FP4, true); else QZ_BIG_DT(QZ_FP4, false);
+    } else {
+      if (dq) QZ_BIG_DT(QZ_NF4, true); else QZ_BIG_DT(QZ_NF4, false);
+    }
+#undef QZ_BIG_DT
+#undef QZ_BIG
     QZ_LAUNCH_CHECK();
     return QZ_OK;
   }

@@ -553,6 +553,23 @@ def test_gemm_prefill(orc, qt, dq, T, M, K):
     assert_close(Y.float().cpu(), Yref, torch.float16, f"gemm {qt} dq={dq} {T}x{M}x{K}")
 
 
+def test_gemm_large_t_tile_bias_and_fp4(orc):
+    """T >= 4096 (the 256 x 256 tile kernel): bias, FP4 without double quant, a
+    partial last token tile, vs the oracle's dequantised weight in fp64."""
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    T, M, K = 4097, 768, 1024
+    W = _w(M, K, seed=41)
+    X = torch.randn(T, K, generator=torch.Generator().manual_seed(42)).to(torch.float16)
+    bias = torch.randn(M, generator=torch.Generator().manual_seed(43)).to(torch.float16)
+    packed, st = quantize_4bit(W.to(DEV), quant_type="fp4", compress_statistics=False)
+    Y = gemm_4bit(X.to(DEV), packed, st, bias=bias.to(DEV), route="fused")
+    o = orc.quantize_4bit(W.float().numpy(), 64, "fp4", double_quant=False)
+    Wd = torch.from_numpy(orc.dequantize(o)).double()
+    Yref = (X.double() @ Wd.t() + bias.double()).numpy()
+    assert_close(Y.float().cpu(), Yref, torch.float16, "gemm 256-tile fp4 + bias")
+
+
 def test_gemm_bias_and_batch_dims(orc):
     from quantizations_amd.core import gemm_4bit, quantize_4bit
 
@@ -572,13 +589,15 @@ def test_gemm_bias_and_batch_dims(orc):
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("qt", ["nf4", "fp4"])
 @pytest.mark.parametrize("dq", [True, False])
-@pytest.mark.parametrize("T,M,K", [(1, 256, 4096), (37, 512, 1024), (64, 4096, 4096), (200, 1024, 2048)])
+@pytest.mark.parametrize("T,M,K", [(1, 256, 4096), (37, 512, 1024), (64, 4096, 4096), (200, 1024, 2048),
+                                   (4100, 520, 1024)])
 def test_gemm_w_operand_is_the_dequantised_weight(qt, dq, dt, T, M, K):
     """One-hot activations read single weights back through the MFMA path: row t
     of Y must equal column k_t of dequantize_4bit(W, out_dtype=dt) BIT FOR BIT
     (values; -0.0 reads back as +0.0).  Pins the in-LDS decode (per-block
     fp16/bf16 table of code*absmax, double-quant rebuild, pair order shared by
-    X and W) to the dequant kernel; covers both token tiles and split-K."""
+    X and W) to the dequant kernel; covers both token tiles, split-K and (T >= 4096)
+    the 256 x 256 tile kernel with partial token and row tiles."""
     from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
 
     W = _w(M, K, seed=3 * T + M)
@@ -593,7 +612,8 @@ def test_gemm_w_operand_is_the_dequantised_weight(qt, dq, dt, T, M, K):
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("T,M,K", [(5, 512, 1024), (64, 4096, 4096), (300, 768, 4096)])
+@pytest.mark.parametrize("T,M,K", [(5, 512, 1024), (64, 4096, 4096), (300, 768, 4096), (4096, 1024, 4096),
+                                   (4352, 264, 512)])
 def test_gemm_random_activations_vs_fp64(dt, T, M, K):
     """Random activations: fused result vs an fp64 matmul of the dequantised
     weight -- only fp32 summation order and the output rounding differ."""

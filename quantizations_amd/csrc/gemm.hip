@@ -237,13 +237,20 @@ constexpr int kBigERow = 144;                       // epilogue image row: 64 ou
 constexpr int kBigMinT = 4096;  // below this the 128-row tile kernel (with split-K) is faster (gemm_micro)
 
 // V (schedule variant, microbenchmark A/B): 0 = decode after the step's MFMAs with a
-// scheduling fence per fragment half; 1 = no fences; 2 = decode between the two k-halves.
+// scheduling fence per fragment half; 1 = no fences; 2 = decode between the two k-halves;
+// 3 = every K-loop global read is an LDS DMA: packed W and its scales land in a 3-deep LDS
+// ring two steps ahead of their decode, which then sits between the step's MFMA halves
+// with no global-load wait; one counted vmcnt per step leaves the newest W DMA in flight.
+constexpr int kBigWp = 8192;                    // V3: packed W of one step (256 rows x 32 B)
+constexpr int kBigWpOff = kBigLds;              // V3: Wp[3]
+constexpr int kBigScOff = kBigWpOff + 3 * kBigWp;  // V3: scale dwords [3][2][256]
+template <int V> constexpr int big_code2_off() { return V == 3 ? kBigScOff + 3 * 2048 : kBigLds; }
 template <int QT, bool DQ, int DT, int V = 0>
 __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kBigLds + (DQ ? 1024 : 0)];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[big_code2_off<V>() + (DQ ? 1024 : 0)];
   typedef __attribute__((address_space(3))) void *lds_ptr_t;
   typedef __attribute__((address_space(1))) void *glb_ptr_t;
-  float *s_code2 = reinterpret_cast<float *>(smem + kBigLds);
+  float *s_code2 = reinterpret_cast<float *>(smem + big_code2_off<V>());
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wt = wave >> 2, wm = wave & 3;
@@ -313,6 +320,49 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
     }
   };
 
+  // V3: W DMA of one step -- thread tid's 16 packed bytes (lane-linear: row tid/2, half tid%2),
+  // and one scale dword per row: threads 0-255 the q dword (DQ; fp32 absmax otherwise), threads
+  // 256-511 the absmax2 entry (DQ; fp32 absmax otherwise) of row tid % 256
+  const int srow = tid & 255;
+  const uint32_t blk_row_s = (uint32_t)(((long long)min(m0 + srow, p.M - 1) * p.K) >> p.bs_log2);
+  auto dma_w = [&](int step, int pb) {
+    const int k0 = step * kBK;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wptr + (k0 >> 1)),
+                                     (lds_ptr_t)(smem + kBigWpOff + pb * kBigWp + wave * 1024), 16, 0, 0);
+    const uint32_t b = blk_row_s + ((uint32_t)k0 >> p.bs_log2);
+    const void *src;
+    if constexpr (DQ) src = tid < 256 ? (const void *)(p.sc.qabsmax + (b & ~3u)) : (const void *)(p.sc.absmax2 + (b >> p.bs2_log2));
+    else src = p.sc.absmax + b;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)src, (lds_ptr_t)(smem + kBigScOff + pb * 2048 + wave * 256), 4, 0, 0);
+  };
+  auto decode_w = [&](int step, int pb, int db) {
+    const v4u wv = *reinterpret_cast<const v4u *>(smem + kBigWpOff + pb * kBigWp + tid * 16);
+    const unsigned char *sc = smem + kBigScOff + pb * 2048;
+    float am;
+    if constexpr (DQ) {
+      const uint32_t b = blk_row + ((uint32_t)(step * kBK) >> p.bs_log2);
+      const uint32_t q = (*reinterpret_cast<const uint32_t *>(sc + wr * 4) >> (8 * (b & 3))) & 255u;
+      am = __fadd_rn(__fmul_rn(s_code2[q], *reinterpret_cast<const float *>(sc + 1024 + wr * 4)), offset);
+    } else {
+      am = *reinterpret_cast<const float *>(sc + 1024 + wr * 4);
+    }
+    WStage st{wv, 0u, am};
+    if constexpr (DQ) {  // store_w rebuilds am from (q, a): pass the rebuilt scale through unchanged
+      uint32_t t[8];
+      block_table<QT, DT>(am, t);
+      const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+      unsigned char *sw = smem + (2 + db) * kBigStage;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint32_t N[4];
+        decode_codes_natural(w[d], t, N);
+        *reinterpret_cast<v4u *>(sw + lds_off(wr, 4 * wh + d)) = v4u{N[0], N[1], N[2], N[3]};
+      }
+    } else {
+      store_w(st, db);
+    }
+  };
+
   f4_t acc[4][8];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -358,6 +408,35 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
   // after X(s+1)'s DMA, multiplies buffer s & 1, then decodes W(s+1) into the other buffer.
   // (A two-set ring needs the loop unrolled by two; its extra live registers spilled the
   // accumulators.)
+  if constexpr (V == 3) {
+    stage_x(0, 0);
+    dma_w(0, 0);
+    if (nsteps > 1) dma_w(1, 1);
+    if (nsteps > 2) dma_w(2, 2);
+    if constexpr (DQ) {
+      if (tid < 256) s_code2[tid] = p.sc.code2[tid];
+      offset = *p.sc.offset;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    decode_w(0, 0, 0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      const bool more = s + 1 < nsteps, w3 = s + 3 < nsteps;
+      if (more) stage_x(s + 1, cur ^ 1);
+      if (w3) dma_w(s + 3, (s + 3) % 3);
+      mfma_half(cur, 0);
+      if (more) decode_w(s + 1, (s + 1) % 3, cur ^ 1);
+      mfma_half(cur, 1);
+      if (more) {  // X(s+1) and W(s+2) landed (only W(s+3)'s two DMAs may still fly), LDS writes done
+        if (w3) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  } else {
   WStage ws;
   stage_x(0, 0);
   load_w(ws, 0);
@@ -382,6 +461,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
       if (V != 2) store_w(ws, cur ^ 1);
       __syncthreads();  // X(s+1) DMA + W(s+1) decode visible to every wave; buffer cur free
     }
+  }
   }
 
   // ---- epilogue: lane holds weight rows 16j + 4*fk + r (r = 0..3) of token 16i + fr ----
@@ -719,7 +799,7 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
     p.ws = nullptr;
     p.k_split = K;
     const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
-#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_big<QT_, DQ_, DT_>), dim3(g), dim3(512), 0, s, p)
+#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_big<QT_, DQ_, DT_, 3>), dim3(g), dim3(512), 0, s, p)
 #define QZ_BIG_DT(QT_, DQ_) \
   do { if (dtype == QZ_DT_F16) QZ_BIG(QT_, DQ_, QZ_DT_F16); else QZ_BIG(QT_, DQ_, QZ_DT_BF16); } while (0)
     if (quant_type == QZ_FP4) {

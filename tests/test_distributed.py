@@ -245,8 +245,18 @@ def _tp_worker(rank, world, port, q, batch=1):
             nxt = out.logits[:, -1:].argmax(-1)
             step = model(input_ids=nxt, past_key_values=out.past_key_values, use_cache=True).logits
             ref_step = ref(input_ids=torch.cat([ids, nxt], 1)).logits[:, -1:]
+            # the bench's decode layout: StaticCache (sized lazily from the local k/v heads) with
+            # explicit cache/position ids, one stream per batch row
+            from transformers.cache_utils import StaticCache
+            cache = StaticCache(config=cfg, max_cache_len=ids.shape[1] + 4)
+            L = ids.shape[1]
+            model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(L), use_cache=True)
+            pos = torch.tensor([L])
+            st_step = model(input_ids=nxt, past_key_values=cache, cache_position=pos,
+                            position_ids=pos.view(1, 1).expand(ids.shape[0], 1), use_cache=True).logits
         rel = float((out.logits - ref_logits).norm() / ref_logits.norm())
-        rel_step = float((step - ref_step).norm() / ref_step.norm())
+        rel_step = max(float((step - ref_step).norm() / ref_step.norm()),
+                       float((st_step - ref_step).norm() / ref_step.norm()))
         o_proj = model.model.layers[0].self_attn.o_proj
         q.put((rank, n, groups, rel, rel_step, isinstance(o_proj, RowParallelLinear4bit),
                model.model.layers[0].self_attn.q_proj.packed.numel()))

@@ -241,10 +241,11 @@ constexpr int kBigMinT = 4096;  // below this the 128-row tile kernel (with spli
 // 3 = every K-loop global read is an LDS DMA: packed W and its scales land in a 3-deep LDS
 // ring two steps ahead of their decode, which then sits between the step's MFMA halves
 // with no global-load wait; one counted vmcnt per step leaves the newest W DMA in flight.
+// 4 = variant 3 without the decode (microbenchmark timing only: wrong results).
 constexpr int kBigWp = 8192;                    // V3: packed W of one step (256 rows x 32 B)
 constexpr int kBigWpOff = kBigLds;              // V3: Wp[3]
 constexpr int kBigScOff = kBigWpOff + 3 * kBigWp;  // V3: scale dwords [3][2][256]
-template <int V> constexpr int big_code2_off() { return V == 3 ? kBigScOff + 3 * 2048 : kBigLds; }
+template <int V> constexpr int big_code2_off() { return V >= 3 ? kBigScOff + 3 * 2048 : kBigLds; }
 template <int QT, bool DQ, int DT, int V = 0>
 __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[big_code2_off<V>() + (DQ ? 1024 : 0)];
@@ -347,7 +348,13 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
       am = *reinterpret_cast<const float *>(sc + 1024 + wr * 4);
     }
     WStage st{wv, 0u, am};
-    if constexpr (DQ) {  // store_w rebuilds am from (q, a): pass the rebuilt scale through unchanged
+    if constexpr (V == 4) {  // microbenchmark ablation: no decode, the packed bytes go to LDS as they are
+      unsigned char *sw = smem + (2 + db) * kBigStage;
+      const uint32_t a = __float_as_uint(am);
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        *reinterpret_cast<v4u *>(sw + lds_off(wr, 4 * wh + d)) = v4u{wv.x ^ a, wv.y, wv.z, wv.w};
+    } else if constexpr (DQ) {  // store_w rebuilds am from (q, a): pass the rebuilt scale through unchanged
       uint32_t t[8];
       block_table<QT, DT>(am, t);
       const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
@@ -408,7 +415,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
   // after X(s+1)'s DMA, multiplies buffer s & 1, then decodes W(s+1) into the other buffer.
   // (A two-set ring needs the loop unrolled by two; its extra live registers spilled the
   // accumulators.)
-  if constexpr (V == 3) {
+  if constexpr (V >= 3) {
     stage_x(0, 0);
     dma_w(0, 0);
     if (nsteps > 1) dma_w(1, 1);

@@ -55,7 +55,7 @@ int main(int argc, char **argv) {
 #define BIGV(V_) vs.push_back({"big256 V=" #V_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
       const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
       hipLaunchKernelGGL((k_gemm_4bit_big<QZ_NF4, true, QZ_DT_F16, V_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { BIGV(0); BIGV(3); }
+    if (T >= 4096) { BIGV(3); BIGV(4); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());

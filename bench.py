@@ -436,6 +436,8 @@ def main():
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
+    ap.add_argument("--no-layer-ops", action="store_true",
+                    help="keep transformers' eager RMSNorm / rotary (8 and 10 launches) instead of layer_ops")
     ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
     ap.add_argument("--tp-mode", choices=("pair", "gather"), default="pair",
                     help="multi-GPU layout: Megatron pairing (column q/k/v/gate/up + row o/down, 2 all-reduces per "
@@ -489,6 +491,10 @@ def main():
     if not args.no_fuse:
         from quantizations_amd.integration import fuse_projection_groups
         n_groups = fuse_projection_groups(model)   # q/k/v and gate/up: one grouped GEMV launch each
+    n_layer_ops = 0
+    if not args.no_layer_ops:
+        from quantizations_amd.integration import fuse_layer_ops
+        n_layer_ops = fuse_layer_ops(model)         # RMSNorm and q/k rotary: one HIP launch each
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 
@@ -562,7 +568,7 @@ def main():
                        "parallelism": ("single" if not sharded else
                                        f"tp{world}-megatron-pair-allreduce" if args.tp_mode == "pair" else
                                        f"tp{world}-rowsplit-allgather"),
-                       "projection_groups": n_groups},
+                       "projection_groups": n_groups, "layer_ops": n_layer_ops},
             "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         print(json.dumps(line), flush=True)

@@ -195,6 +195,28 @@ int qz_bench_read_floor(const void *p, long long bytes, unsigned int *sink, void
  * period every dependent launch on a stream pays (dispatch + end of kernel). */
 int qz_bench_empty(unsigned int *sink, void *stream);
 
+/* ---- the Linear4bit's callers in a Llama decoder layer (integration.fuse_layer_ops) ----
+ * Neither op is in the reference (it leaves them to transformers); they are
+ * one-launch restatements of the torch code around the 4-bit projections, with
+ * torch's fp32 opmath and its per-op rounding, so that a decode step is not
+ * dominated by ~8 small launches per norm and ~10 per rotary application. */
+
+/* LlamaRMSNorm.forward (transformers modeling_llama.py:62-67) over `rows` rows
+ * of K elements: h = fp32(x); var = sum(h*h) * (1/K); h *= rsqrt(var + eps);
+ * y = weight * round_to_dtype(h) (fp32 product, rounded to `dtype`).  x, weight
+ * and y share `dtype`; row strides ldx/ldy are in elements. */
+int qz_rmsnorm(const void *x, int dtype, long long rows, int K, long long ldx, const void *weight, float eps, void *y,
+               long long ldy, void *stream);
+
+/* apply_rotary_pos_emb (modeling_llama.py:130-160) for q AND k in one launch:
+ * out = x*cos + rotate_half(x)*sin, each product and the sum rounded to `dtype`
+ * as torch does.  q/k are [B, H, S, D] with element strides (b, h, s) given in
+ * q_str/k_str (d contiguous); outputs use qo_str/ko_str; cos/sin are [B, S, D]
+ * with strides cs_str (b, s) (stride 0 broadcasts).  D must be even. */
+int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long long *q_str, void *q_out,
+               const long long *qo_str, const void *k, int Hk, const long long *k_str, void *k_out,
+               const long long *ko_str, const void *cos, const void *sin, const long long *cs_str, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

@@ -1,0 +1,167 @@
+// layer_ops.hip -- the two small ops that sit around the 4-bit projections of a
+// Llama decoder layer, each as ONE launch (integration.fuse_layer_ops):
+//
+//  * RMSNorm, which feeds q/k/v and gate/up (modeling_llama.py:62-67).  In eager
+//    torch it is 8 launches (cast, pow, mean, add, rsqrt, mul, cast, mul);
+//  * rotary position embedding of q and k (modeling_llama.py:130-160), ~10
+//    launches (2 x {mul, slice-neg, cat, mul, add}).
+//
+// At batch-1 decode each of those launches moves a few KiB, so the step is
+// bound by the fixed cost of a dependent launch (~1.55 us), not
+// by bytes.  Numerics follow torch's elementwise opmath exactly: fp32 compute,
+// rounding to the storage dtype after every op that torch stores.  The only
+// freedom taken is RMSNorm's fp32 sum order (torch's reduction tree is not
+// specified), so RMSNorm is checked to a tolerance and rotary bit-exactly.
+#include "common.h"
+
+namespace qz {
+namespace {
+
+template <int DT> __device__ __forceinline__ float round_dt(float v) {
+  if constexpr (DT == QZ_DT_F16) return __half2float(__float2half_rn(v));
+  else if constexpr (DT == QZ_DT_BF16) return __bfloat162float(__float2bfloat16(v));
+  else return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// One 256-thread workgroup per row.  VEC: 16-B loads of 16 / sizeof(elem)
+// elements (host-checked alignment, K a multiple of the vector width); the
+// second pass re-reads x from L1/L2 (8 KiB per fp16 Llama-3-8B row).
+template <int DT, bool VEC>
+__global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, int K, long long ldx,
+                                                 const void *__restrict__ w, float eps, void *__restrict__ y,
+                                                 long long ldy) {
+  constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
+  constexpr int V = VEC ? 16 / ES : 1;
+  __shared__ float s_part[4];
+  const long long row = blockIdx.x;
+  const char *xr = reinterpret_cast<const char *>(x) + row * ldx * ES;
+  char *yr = reinterpret_cast<char *>(y) + row * ldy * ES;
+  const int nv = K / V;
+
+  float ss = 0.0f;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float h = load_f32<DT>(xr, (long long)i * V + j);
+      ss = __fadd_rn(ss, __fmul_rn(h, h));
+    }
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = __fadd_rn(__fadd_rn(s_part[0], s_part[1]), __fadd_rn(s_part[2], s_part[3]));
+  // torch MeanOps: sum * (1/N) in fp32; then rsqrt(var + eps)
+  const float r = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)K), eps));
+  for (int i = threadIdx.x; i < nv; i += 256) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const long long e = (long long)i * V + j;
+      const float h = round_dt<DT>(__fmul_rn(load_f32<DT>(xr, e), r));  // hidden.to(input_dtype)
+      store_f32<DT>(yr, e, __fmul_rn(load_f32<DT>(w, e), h));         // weight * hidden
+    }
+  }
+}
+
+struct RopeArgs {
+  const void *x[2];
+  void *o[2];
+  long long xs[2][3], os[2][3];  // (b, h, s) element strides
+  int H[2];
+  long long rows_q;              // B*Hq*S: rows of q, then B*Hk*S rows of k
+  long long pairs;               // total (row, d < D/2) pairs
+  const void *cos, *sin;
+  long long cb, cs;
+  int S, half;
+};
+
+// One thread per (row, d) pair: it writes out[d] and out[d + D/2].
+template <int DT>
+__global__ __launch_bounds__(256) void k_rope_qk(RopeArgs a) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.pairs) return;
+  const long long row_all = idx / a.half;
+  const int d = (int)(idx - row_all * a.half);
+  const int t = row_all >= a.rows_q ? 1 : 0;
+  const long long row = row_all - (t ? a.rows_q : 0);
+  const int H = a.H[t];
+  const long long s = row % a.S, bh = row / a.S, h = bh % H, b = bh / H;
+  const long long xo = b * a.xs[t][0] + h * a.xs[t][1] + s * a.xs[t][2] + d;
+  const long long oo = b * a.os[t][0] + h * a.os[t][1] + s * a.os[t][2] + d;
+  const long long co = b * a.cb + s * a.cs + d;
+  const float x1 = load_f32<DT>(a.x[t], xo), x2 = load_f32<DT>(a.x[t], xo + a.half);
+  const float c1 = load_f32<DT>(a.cos, co), c2 = load_f32<DT>(a.cos, co + a.half);
+  const float s1 = load_f32<DT>(a.sin, co), s2 = load_f32<DT>(a.sin, co + a.half);
+  // q*cos + cat(-x2, x1)*sin, every torch op rounded to the storage dtype
+  const float lo = __fadd_rn(round_dt<DT>(__fmul_rn(x1, c1)), round_dt<DT>(__fmul_rn(-x2, s1)));
+  const float hi = __fadd_rn(round_dt<DT>(__fmul_rn(x2, c2)), round_dt<DT>(__fmul_rn(x1, s2)));
+  store_f32<DT>(a.o[t], oo, lo);
+  store_f32<DT>(a.o[t], oo + a.half, hi);
+}
+
+template <int DT>
+void launch_rmsnorm(bool vec, long long rows, const void *x, int K, long long ldx, const void *w, float eps, void *y,
+                    long long ldy, hipStream_t s) {
+  if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true>), dim3((unsigned)rows), dim3(256), 0, s, x, K, ldx, w, eps, y, ldy);
+  else hipLaunchKernelGGL((k_rmsnorm<DT, false>), dim3((unsigned)rows), dim3(256), 0, s, x, K, ldx, w, eps, y, ldy);
+}
+
+}  // namespace
+}  // namespace qz
+
+using namespace qz;
+
+extern "C" int qz_rmsnorm(const void *x, int dtype, long long rows, int K, long long ldx, const void *weight,
+                          float eps, void *y, long long ldy, void *stream) {
+  if (rows < 0 || K < 0) return QZ_ERR_ARG;
+  if (rows == 0 || K == 0) return 0;
+  if (!x || !weight || !y || ldx < K || ldy < K) return QZ_ERR_ARG;
+  if (rows > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  const int es = dtype == QZ_DT_F32 ? 4 : 2;
+  const int v = 16 / es;
+  const bool vec = K % v == 0 && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)x | (uintptr_t)y | (uintptr_t)weight) % 16 == 0;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case QZ_DT_F16: launch_rmsnorm<QZ_DT_F16>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
+    case QZ_DT_BF16: launch_rmsnorm<QZ_DT_BF16>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
+    case QZ_DT_F32: launch_rmsnorm<QZ_DT_F32>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long long *q_str, void *q_out,
+                          const long long *qo_str, const void *k, int Hk, const long long *k_str, void *k_out,
+                          const long long *ko_str, const void *cos, const void *sin, const long long *cs_str,
+                          void *stream) {
+  if (B < 0 || S < 0 || D < 0 || Hq < 0 || Hk < 0) return QZ_ERR_ARG;
+  if ((D & 1) != 0) return QZ_ERR_SHAPE;
+  if (B == 0 || S == 0 || D == 0 || Hq + Hk == 0) return 0;
+  if (!q_str || !qo_str || !k_str || !ko_str || !cs_str || !cos || !sin) return QZ_ERR_ARG;
+  if ((Hq > 0 && (!q || !q_out)) || (Hk > 0 && (!k || !k_out))) return QZ_ERR_ARG;
+  RopeArgs a{};
+  a.x[0] = q; a.x[1] = k; a.o[0] = q_out; a.o[1] = k_out;
+  for (int i = 0; i < 3; ++i) {
+    a.xs[0][i] = q_str[i]; a.os[0][i] = qo_str[i]; a.xs[1][i] = k_str[i]; a.os[1][i] = ko_str[i];
+  }
+  a.H[0] = Hq; a.H[1] = Hk;
+  a.rows_q = (long long)B * Hq * S;
+  a.half = D / 2;
+  a.pairs = (a.rows_q + (long long)B * Hk * S) * a.half;
+  a.cos = cos; a.sin = sin; a.cb = cs_str[0]; a.cs = cs_str[1]; a.S = S;
+  const long long blocks = (a.pairs + 255) / 256;
+  if (blocks > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case QZ_DT_F16: hipLaunchKernelGGL((k_rope_qk<QZ_DT_F16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case QZ_DT_BF16: hipLaunchKernelGGL((k_rope_qk<QZ_DT_BF16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case QZ_DT_F32: hipLaunchKernelGGL((k_rope_qk<QZ_DT_F32>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}

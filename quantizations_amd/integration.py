@@ -124,6 +124,74 @@ def unfuse_projection_groups(model: nn.Module) -> None:
 
 
 # ---------------------------------------------------------------------------
+# the Linear4bit's neighbours in a decoder layer: RMSNorm and rotary embedding
+# ---------------------------------------------------------------------------
+
+# norms whose forward is exactly LlamaRMSNorm's (modeling_llama.py:62-67)
+RMSNORM_CLASSES = ("LlamaRMSNorm", "MistralRMSNorm", "Qwen2RMSNorm")
+_ROPE_PATCHED = {}  # module name -> original apply_rotary_pos_emb
+
+
+def _fused_rmsnorm_forward(mod: nn.Module, orig):
+    from .layer_ops import rms_norm, rms_norm_supported
+
+    def forward(hidden_states: torch.Tensor) -> torch.Tensor:
+        if rms_norm_supported(hidden_states, mod.weight):
+            return rms_norm(hidden_states, mod.weight, mod.variance_epsilon)
+        return orig(hidden_states)  # transformers' own eager code (e.g. CPU tensors, mixed dtypes)
+    return forward
+
+
+def _fused_rope(orig):
+    from .layer_ops import rope_qk, rope_supported
+
+    def apply_rotary_pos_emb(q, k, cos, sin, unsqueeze_dim=1, **kw):
+        if not kw and rope_supported(q, k, cos, sin, unsqueeze_dim):
+            return rope_qk(q, k, cos, sin)
+        return orig(q, k, cos, sin, unsqueeze_dim, **kw)
+    apply_rotary_pos_emb._qz_orig = orig
+    return apply_rotary_pos_emb
+
+
+def fuse_layer_ops(model: nn.Module) -> int:
+    """Route every Llama-style RMSNorm of `model` and the rotary embedding of its
+    attention modules through one HIP launch each (layer_ops.rms_norm /
+    rope_qk) instead of transformers' 8- and 10-launch eager forms.  Inputs the
+    kernels do not take keep the original code.  Returns the number of modules
+    patched (norms + modeling modules whose apply_rotary_pos_emb was replaced)."""
+    import sys
+
+    n = 0
+    for m in model.modules():
+        name = type(m).__name__
+        if name in RMSNORM_CLASSES and "forward" not in m.__dict__ and hasattr(m, "variance_epsilon"):
+            m.__dict__["forward"] = _fused_rmsnorm_forward(m, m.forward)
+            m.__dict__["_qz_fused_norm"] = True
+            n += 1
+        elif name.endswith("Attention"):
+            modname = type(m).__module__
+            mod = sys.modules.get(modname)
+            fn = getattr(mod, "apply_rotary_pos_emb", None)
+            if fn is not None and modname not in _ROPE_PATCHED:
+                _ROPE_PATCHED[modname] = fn
+                mod.apply_rotary_pos_emb = _fused_rope(fn)
+                n += 1
+    return n
+
+
+def unfuse_layer_ops(model: nn.Module) -> None:
+    """Undo fuse_layer_ops (norm forwards and every patched apply_rotary_pos_emb)."""
+    import sys
+
+    for m in model.modules():
+        if m.__dict__.pop("_qz_fused_norm", None):
+            m.__dict__.pop("forward", None)
+    for modname, fn in list(_ROPE_PATCHED.items()):
+        setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)
+        del _ROPE_PATCHED[modname]
+
+
+# ---------------------------------------------------------------------------
 # pre-quantised checkpoints (SURVEY.md 8f row 1)
 # ---------------------------------------------------------------------------
 

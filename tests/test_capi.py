@@ -61,3 +61,11 @@ def test_argument_errors_are_reported_not_launched():
     assert L.qz_quantize_4bit(1, 9, 64, 64, 0, 1, 1, 0) == -4
     assert L.qz_gemv_4bit(4, 64, 1, 0, 1, 0, 64, 1, 1, 1, 1, 1, 256, 0, 0, 0, 1, 0) == -1  # both scale sources
     assert L.cgemm_4bit_inference_naive_fp32(8, 2, 64, 1, 1, 1, 1, 1, 8, 32, 8, 64) == -3  # n != 1
+    # layer ops: negative sizes / odd head_dim are rejected before any launch
+    assert L.qz_rmsnorm(1, 0, -1, 64, 64, 1, 1e-6, 1, 64, 0) == -1
+    assert L.qz_rmsnorm(1, 0, 4, 64, 32, 1, 1e-6, 1, 64, 0) == -1  # ldx < K
+    assert L.qz_rmsnorm(1, 0, 0, 64, 64, 1, 1e-6, 1, 64, 0) == 0    # empty: nothing to do
+    s3 = (ctypes.c_longlong * 3)(0, 0, 0)
+    s2 = (ctypes.c_longlong * 2)(0, 0)
+    assert L.qz_rope_qk(0, 1, 1, 127, 1, 1, s3, 1, s3, 1, 1, s3, 1, s3, 1, 1, s2, 0) == -3
+    assert L.qz_rope_qk(0, 1, 1, 128, 1, 1, s3, 1, s3, 1, 1, s3, 1, s3, 0, 1, s2, 0) == -1

@@ -91,3 +91,34 @@ def test_replace_with_bnb_linear_skips_lm_head_on_meta():
     replace_with_bnb_linear(t, quant_type="nf4", device="meta")
     assert isinstance(t.proj, qa.Linear4bit) and not isinstance(t.lm_head, qa.Linear4bit)
     assert t.proj.weight.quant_type == "nf4" and t.proj.weight.compress_statistics
+
+
+def test_fuse_layer_ops_patches_and_restores_on_cpu():
+    """fuse_layer_ops installs the HIP norm/rotary forms; on CPU tensors the kernels
+    do not apply and transformers' own code runs, so logits are unchanged; unfuse
+    restores the original forwards and apply_rotary_pos_emb."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    import transformers.models.llama.modeling_llama as ml
+
+    from quantizations_amd.integration import fuse_layer_ops, unfuse_layer_ops
+    from quantizations_amd.layer_ops import rms_norm_supported, rope_supported
+
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=97)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).eval()
+    ids = torch.randint(0, 97, (1, 5))
+    orig = ml.apply_rotary_pos_emb
+    with torch.no_grad():
+        ref = model(input_ids=ids).logits
+        assert fuse_layer_ops(model) == 2 * 2 + 1 + 1
+        assert ml.apply_rotary_pos_emb is not orig and ml.apply_rotary_pos_emb._qz_orig is orig
+        assert fuse_layer_ops(model) == 0  # idempotent
+        assert torch.equal(model(input_ids=ids).logits, ref)
+        unfuse_layer_ops(model)
+    assert ml.apply_rotary_pos_emb is orig
+    assert not any("forward" in m.__dict__ for m in model.modules())
+    x = torch.randn(2, 64)
+    assert not rms_norm_supported(x, torch.ones(64))  # CPU tensors never reach the kernel
+    q = torch.randn(1, 4, 3, 16)
+    assert not rope_supported(q, q, torch.randn(1, 3, 16), torch.randn(1, 3, 16))

@@ -55,6 +55,7 @@ MODELS = {"llama3-8b": LLAMA3_8B, "llama3-70b": LLAMA3_70B}
 LAYER_SHAPES = [(4096, 4096), (1024, 4096), (1024, 4096), (4096, 4096), (14336, 4096), (14336, 4096), (4096, 14336)]
 GEMV_BYTES_4096 = 8_672_324  # packed 8,388,608 + qabsmax 262,144 + absmax2 4,096 + offset 4 + code2 1,024 + LUT 64
 #                              + x 8,192 + y 8,192   
+CAPTURE_MODE = "thread_local"  # bench --capture-mode (the RCCL watchdog thread queries events during capture)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -147,7 +148,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
             step()
     torch.cuda.current_stream().wait_stream(s)
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
         step()
     for _ in range(warmup):
         graph.replay()
@@ -438,6 +439,10 @@ def main():
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--no-layer-ops", action="store_true",
                     help="keep transformers' eager RMSNorm / rotary (8 and 10 launches) instead of layer_ops")
+    ap.add_argument("--layer-ops", choices=("all", "norm", "rope", "none"), default="all",
+                    help="which transformers ops integration.fuse_layer_ops replaces")
+    ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
+                    help="torch.cuda.graph capture_error_mode of the decode-step capture")
     ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
     ap.add_argument("--tp-mode", choices=("pair", "gather"), default="pair",
                     help="multi-GPU layout: Megatron pairing (column q/k/v/gate/up + row o/down, 2 all-reduces per "
@@ -449,6 +454,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="N > 1: keep the global batch at --batch (one bs=1 stream served by all N GPUs)")
     args = ap.parse_args()
+    global CAPTURE_MODE
+    CAPTURE_MODE = args.capture_mode
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -492,9 +499,10 @@ def main():
         from quantizations_amd.integration import fuse_projection_groups
         n_groups = fuse_projection_groups(model)   # q/k/v and gate/up: one grouped GEMV launch each
     n_layer_ops = 0
-    if not args.no_layer_ops:
+    if not args.no_layer_ops and args.layer_ops != "none":
         from quantizations_amd.integration import fuse_layer_ops
-        n_layer_ops = fuse_layer_ops(model)         # RMSNorm and q/k rotary: one HIP launch each
+        n_layer_ops = fuse_layer_ops(model, norm=args.layer_ops in ("all", "norm"),
+                                     rope=args.layer_ops in ("all", "rope"))  # one HIP launch each
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 

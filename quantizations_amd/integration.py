@@ -153,7 +153,7 @@ def _fused_rope(orig):
     return apply_rotary_pos_emb
 
 
-def fuse_layer_ops(model: nn.Module) -> int:
+def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True) -> int:
     """Route every Llama-style RMSNorm of `model` and the rotary embedding of its
     attention modules through one HIP launch each (layer_ops.rms_norm /
     rope_qk) instead of transformers' 8- and 10-launch eager forms.  Inputs the
@@ -164,11 +164,11 @@ def fuse_layer_ops(model: nn.Module) -> int:
     n = 0
     for m in model.modules():
         name = type(m).__name__
-        if name in RMSNORM_CLASSES and "forward" not in m.__dict__ and hasattr(m, "variance_epsilon"):
+        if norm and name in RMSNORM_CLASSES and "forward" not in m.__dict__ and hasattr(m, "variance_epsilon"):
             m.__dict__["forward"] = _fused_rmsnorm_forward(m, m.forward)
             m.__dict__["_qz_fused_norm"] = True
             n += 1
-        elif name.endswith("Attention"):
+        elif rope and name.endswith("Attention"):
             modname = type(m).__module__
             mod = sys.modules.get(modname)
             fn = getattr(mod, "apply_rotary_pos_emb", None)

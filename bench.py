@@ -439,7 +439,7 @@ def main():
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--no-layer-ops", action="store_true",
                     help="keep transformers' eager RMSNorm / rotary (8 and 10 launches) instead of layer_ops")
-    ap.add_argument("--layer-ops", choices=("all", "norm", "rope", "none"), default="all",
+    ap.add_argument("--layer-ops", choices=("all", "norm", "rope", "mlp", "none"), default="all",
                     help="which transformers ops integration.fuse_layer_ops replaces")
     ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
                     help="torch.cuda.graph capture_error_mode of the decode-step capture")
@@ -502,7 +502,8 @@ def main():
     if not args.no_layer_ops and args.layer_ops != "none":
         from quantizations_amd.integration import fuse_layer_ops
         n_layer_ops = fuse_layer_ops(model, norm=args.layer_ops in ("all", "norm"),
-                                     rope=args.layer_ops in ("all", "rope"))  # one HIP launch each
+                                     rope=args.layer_ops in ("all", "rope"),
+                                     mlp=args.layer_ops in ("all", "mlp"))  # one HIP launch each
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 

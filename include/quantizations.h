@@ -217,6 +217,11 @@ int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long
                const long long *qo_str, const void *k, int Hk, const long long *k_str, void *k_out,
                const long long *ko_str, const void *cos, const void *sin, const long long *cs_str, void *stream);
 
+/* LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) for hidden_act "silu"
+ * (modeling_llama.py:175): y = round(round(g / (1 + exp(-g))) * u) over n
+ * contiguous elements of `dtype` (torch's two rounded elementwise ops). */
+int qz_silu_mul(const void *gate, const void *up, int dtype, long long n, void *y, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

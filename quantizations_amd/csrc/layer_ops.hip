@@ -1,10 +1,11 @@
-// layer_ops.hip -- the two small ops that sit around the 4-bit projections of a
+// layer_ops.hip -- the small ops that sit around the 4-bit projections of a
 // Llama decoder layer, each as ONE launch (integration.fuse_layer_ops):
 //
 //  * RMSNorm, which feeds q/k/v and gate/up (modeling_llama.py:62-67).  In eager
 //    torch it is 8 launches (cast, pow, mean, add, rsqrt, mul, cast, mul);
 //  * rotary position embedding of q and k (modeling_llama.py:130-160), ~10
-//    launches (2 x {mul, slice-neg, cat, mul, add}).
+//    launches (2 x {mul, slice-neg, cat, mul, add});
+//  * SiLU(gate) * up, the input of down_proj (modeling_llama.py:175), 2 launches.
 //
 // At batch-1 decode each of those launches moves a few KiB, so the step is
 // bound by the fixed cost of a dependent launch (~1.55 us), not
@@ -104,6 +105,19 @@ __global__ __launch_bounds__(256) void k_rope_qk(RopeArgs a) {
   store_f32<DT>(a.o[t], oo + a.half, hi);
 }
 
+// LlamaMLP's act_fn(gate) * up (modeling_llama.py:175) for hidden_act "silu":
+// torch's silu is x / (1 + exp(-x)) in fp32, rounded to the storage dtype, then
+// the product of the two stored values rounded again.  One thread per element.
+template <int DT>
+__global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, const void *__restrict__ u, long long n,
+                                                  void *__restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float x = load_f32<DT>(g, i);
+  const float a = round_dt<DT>(__fdiv_rn(x, __fadd_rn(1.0f, expf(-x))));
+  store_f32<DT>(y, i, __fmul_rn(a, load_f32<DT>(u, i)));
+}
+
 template <int DT>
 void launch_rmsnorm(bool vec, long long rows, const void *x, int K, long long ldx, const void *w, float eps, void *y,
                     long long ldy, hipStream_t s) {
@@ -161,6 +175,23 @@ extern "C" int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq,
     case QZ_DT_F16: hipLaunchKernelGGL((k_rope_qk<QZ_DT_F16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
     case QZ_DT_BF16: hipLaunchKernelGGL((k_rope_qk<QZ_DT_BF16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
     case QZ_DT_F32: hipLaunchKernelGGL((k_rope_qk<QZ_DT_F32>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_silu_mul(const void *gate, const void *up, int dtype, long long n, void *y, void *stream) {
+  if (n < 0) return QZ_ERR_ARG;
+  if (n == 0) return 0;
+  if (!gate || !up || !y) return QZ_ERR_ARG;
+  const long long blocks = (n + 255) / 256;
+  if (blocks > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)blocks), blk(256);
+  switch (dtype) {
+    case QZ_DT_F16: hipLaunchKernelGGL((k_silu_mul<QZ_DT_F16>), grid, blk, 0, s, gate, up, n, y); break;
+    case QZ_DT_BF16: hipLaunchKernelGGL((k_silu_mul<QZ_DT_BF16>), grid, blk, 0, s, gate, up, n, y); break;
+    case QZ_DT_F32: hipLaunchKernelGGL((k_silu_mul<QZ_DT_F32>), grid, blk, 0, s, gate, up, n, y); break;
     default: return QZ_ERR_DTYPE;
   }
   return (int)hipGetLastError();

@@ -129,6 +129,8 @@ def unfuse_projection_groups(model: nn.Module) -> None:
 
 # norms whose forward is exactly LlamaRMSNorm's (modeling_llama.py:62-67)
 RMSNORM_CLASSES = ("LlamaRMSNorm", "MistralRMSNorm", "Qwen2RMSNorm")
+# MLPs whose forward is down_proj(act_fn(gate_proj(x)) * up_proj(x)) (modeling_llama.py:174-176)
+MLP_CLASSES = ("LlamaMLP", "MistralMLP", "Qwen2MLP")
 _ROPE_PATCHED = {}  # module name -> original apply_rotary_pos_emb
 
 
@@ -153,12 +155,24 @@ def _fused_rope(orig):
     return apply_rotary_pos_emb
 
 
-def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True) -> int:
-    """Route every Llama-style RMSNorm of `model` and the rotary embedding of its
-    attention modules through one HIP launch each (layer_ops.rms_norm /
-    rope_qk) instead of transformers' 8- and 10-launch eager forms.  Inputs the
-    kernels do not take keep the original code.  Returns the number of modules
-    patched (norms + modeling modules whose apply_rotary_pos_emb was replaced)."""
+def _fused_mlp_forward(mod: nn.Module):
+    from .layer_ops import silu_mul, silu_mul_supported
+
+    def forward(x: torch.Tensor) -> torch.Tensor:
+        g = mod.gate_proj(x)  # same call order as LlamaMLP.forward (a DecodeGroup launches gate+up here)
+        u = mod.up_proj(x)
+        h = silu_mul(g, u) if silu_mul_supported(g, u) else mod.act_fn(g) * u
+        return mod.down_proj(h)
+    return forward
+
+
+def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True) -> int:
+    """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
+    attention modules and the SiLU-gate product of its MLPs through one HIP
+    launch each (layer_ops.rms_norm / rope_qk / silu_mul) instead of
+    transformers' 8-, 10- and 2-launch eager forms.  Inputs the kernels do not
+    take keep the original code.  Returns the number of modules patched (norms,
+    MLPs, and modeling modules whose apply_rotary_pos_emb was replaced)."""
     import sys
 
     n = 0
@@ -167,6 +181,12 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True) -> in
         if norm and name in RMSNORM_CLASSES and "forward" not in m.__dict__ and hasattr(m, "variance_epsilon"):
             m.__dict__["forward"] = _fused_rmsnorm_forward(m, m.forward)
             m.__dict__["_qz_fused_norm"] = True
+            n += 1
+        elif mlp and name in MLP_CLASSES and "forward" not in m.__dict__ and \
+                "silu" in type(getattr(m, "act_fn", None)).__name__.lower() and \
+                all(hasattr(m, p) for p in ("gate_proj", "up_proj", "down_proj")):
+            m.__dict__["forward"] = _fused_mlp_forward(m)
+            m.__dict__["_qz_fused_mlp"] = True
             n += 1
         elif rope and name.endswith("Attention"):
             modname = type(m).__module__
@@ -184,7 +204,7 @@ def unfuse_layer_ops(model: nn.Module) -> None:
     import sys
 
     for m in model.modules():
-        if m.__dict__.pop("_qz_fused_norm", None):
+        if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None):
             m.__dict__.pop("forward", None)
     for modname, fn in list(_ROPE_PATCHED.items()):
         setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)

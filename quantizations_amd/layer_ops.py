@@ -1,13 +1,15 @@
-"""One-launch HIP forms of the two small ops around a Llama layer's 4-bit
+"""One-launch HIP forms of the small ops around a Llama layer's 4-bit
 projections (csrc/layer_ops.hip, C-ABI include/quantizations.h):
 
 * ``rms_norm``  -- LlamaRMSNorm.forward (transformers modeling_llama.py:62-67),
   which produces the input of q/k/v and gate/up;
 * ``rope_qk``   -- apply_rotary_pos_emb (modeling_llama.py:138-160), applied to
-  the outputs of q_proj/k_proj.
+  the outputs of q_proj/k_proj;
+* ``silu_mul``  -- LlamaMLP's act_fn(gate_proj(x)) * up_proj(x)
+  (modeling_llama.py:175), the input of down_proj.
 
-Neither is in the reference (it leaves them to transformers).  They exist
-because at batch-1 decode the eager torch forms cost ~8 and ~10 dependent
+None of them is in the reference (it leaves them to transformers).  They exist
+because at batch-1 decode the eager torch forms cost ~8, ~10 and 2 dependent
 launches per call, which dominate the step once the Linear4bit GEMVs are
 fused.  ``integration.fuse_layer_ops`` installs them.
 No CPU or torch fallback lives here: the callers decide what is supported.
@@ -83,3 +85,18 @@ def rope_qk(q: torch.Tensor, k: torch.Tensor, cos: torch.Tensor, sin: torch.Tens
                                    cos.data_ptr(), sin.data_ptr(), cs, _lib.stream_of(q)),
                "qz_rope_qk")
     return qo, ko
+
+
+def silu_mul_supported(g: torch.Tensor, u: torch.Tensor) -> bool:
+    return (g.is_cuda and g.dtype in _SUPPORTED and u.dtype == g.dtype and u.device == g.device
+            and g.shape == u.shape and g.is_contiguous() and u.is_contiguous())
+
+
+def silu_mul(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """F.silu(g) * u with torch's per-op rounding, one launch."""
+    if not silu_mul_supported(g, u):
+        raise ValueError("silu_mul: unsupported shapes/dtypes/layout")
+    y = torch.empty_like(g)
+    _lib.check(_lib.lib.qz_silu_mul(g.data_ptr(), u.data_ptr(), _lib.dtype_code(g.dtype), g.numel(), y.data_ptr(),
+                                    _lib.stream_of(g)), "qz_silu_mul")
+    return y

@@ -10,6 +10,8 @@ Bars:
     LlamaRMSNorm.forward -- a 1-ulp change of the rounded normalised value,
     times the weight, rounded again -- and >= 99 % of elements bit-identical
     (fp16/bf16); fp32 outputs within 4 ulp.
+  * silu_mul: vs F.silu(g) * u, >= 99 % bit-identical, all within 2 ulp
+    (torch's and the kernel's expf may differ in the last place).
   * tiny Llama with fuse_layer_ops: greedy tokens identical to the unfused
     model, logits rel. err. <= 2e-3, also under HIP-graph capture.
 """
@@ -98,6 +100,21 @@ def test_rope_qk_bit_exact_vs_apply_rotary_pos_emb(dtype, B, Hq, Hk, S, D, bcast
     assert qo.stride() == q.stride()  # torch's elementwise ops keep the transposed layout too
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(1, 1, 14336), (4, 1, 14336), (2, 9, 1000), (3, 333)])
+def test_silu_mul_vs_torch(dtype, shape):
+    from quantizations_amd.layer_ops import silu_mul
+
+    g = (torch.randn(shape, device=DEV) * 4).to(dtype)
+    u = (torch.randn(shape, device=DEV) * 4).to(dtype)
+    ref = torch.nn.functional.silu(g) * u
+    y = silu_mul(g, u)
+    # bit-exact where the device expf agrees with torch's; at most 1 ulp of silu(g) (times u) otherwise
+    d = (y.double() - ref.double()).abs()
+    assert bool((d <= 2 * _ulp_at(ref, dtype) + 1e-30).all()), float(d.max())
+    assert (y == ref).float().mean().item() >= 0.99
+
+
 def _tiny_llama(seed=3):
     from transformers import LlamaConfig, LlamaForCausalLM
 
@@ -159,7 +176,7 @@ def test_tiny_llama_fuse_layer_ops_decode_and_graph():
         ref_toks, ref_logits = greedy(6)
         ref_graph = graph_logits(ref_toks[:, :1])
         n = fuse_layer_ops(model)
-        assert n == 2 * cfg.num_hidden_layers + 1 + 1  # 2 norms per layer + final norm + one modeling module
+        assert n == 3 * cfg.num_hidden_layers + 1 + 1  # 2 norms + 1 MLP per layer, final norm, one modeling module
         toks, logits = greedy(6)
         assert torch.equal(toks, ref_toks)
         for a, b in zip(logits, ref_logits):

@@ -439,7 +439,7 @@ def main():
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--no-layer-ops", action="store_true",
                     help="keep transformers' eager RMSNorm / rotary (8 and 10 launches) instead of layer_ops")
-    ap.add_argument("--layer-ops", choices=("all", "norm", "rope", "mlp", "none"), default="all",
+    ap.add_argument("--layer-ops", choices=("all", "all+decoder", "norm", "rope", "mlp", "none"), default="all",
                     help="which transformers ops integration.fuse_layer_ops replaces")
     ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
                     help="torch.cuda.graph capture_error_mode of the decode-step capture")
@@ -501,9 +501,10 @@ def main():
     n_layer_ops = 0
     if not args.no_layer_ops and args.layer_ops != "none":
         from quantizations_amd.integration import fuse_layer_ops
-        n_layer_ops = fuse_layer_ops(model, norm=args.layer_ops in ("all", "norm"),
-                                     rope=args.layer_ops in ("all", "rope"),
-                                     mlp=args.layer_ops in ("all", "mlp"))  # one HIP launch each
+        n_layer_ops = fuse_layer_ops(model, norm=args.layer_ops in ("all", "all+decoder", "norm"),
+                                     rope=args.layer_ops in ("all", "all+decoder", "rope"),
+                                     mlp=args.layer_ops in ("all", "all+decoder", "mlp"),
+                                     decoder=args.layer_ops == "all+decoder")  # one HIP launch each
     log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
         f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
 

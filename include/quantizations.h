@@ -208,6 +208,13 @@ int qz_bench_empty(unsigned int *sink, void *stream);
 int qz_rmsnorm(const void *x, int dtype, long long rows, int K, long long ldx, const void *weight, float eps, void *y,
                long long ldy, void *stream);
 
+/* `residual + x` followed by the RMSNorm above (LlamaDecoderLayer.forward:317-321)
+ * in one launch: sum = round_to_dtype(residual + x) is stored (the new residual
+ * stream) and y = rmsnorm(sum).  residual shares x's row stride ldx; sum and y
+ * use ldy. */
+int qz_add_rmsnorm(const void *x, const void *residual, int dtype, long long rows, int K, long long ldx,
+                   const void *weight, float eps, void *sum, void *y, long long ldy, void *stream);
+
 /* apply_rotary_pos_emb (modeling_llama.py:130-160) for q AND k in one launch:
  * out = x*cos + rotate_half(x)*sin, each product and the sum rounded to `dtype`
  * as torch does.  q/k are [B, H, S, D] with element strides (b, h, s) given in

@@ -5,7 +5,8 @@
 //    torch it is 8 launches (cast, pow, mean, add, rsqrt, mul, cast, mul);
 //  * rotary position embedding of q and k (modeling_llama.py:130-160), ~10
 //    launches (2 x {mul, slice-neg, cat, mul, add});
-//  * SiLU(gate) * up, the input of down_proj (modeling_llama.py:175), 2 launches.
+//  * SiLU(gate) * up, the input of down_proj (modeling_llama.py:175), 2 launches;
+//  * residual add + post-attention RMSNorm (LlamaDecoderLayer.forward:317-321).
 //
 // At batch-1 decode each of those launches moves a few KiB, so the step is
 // bound by the fixed cost of a dependent launch (~1.55 us), not
@@ -33,23 +34,32 @@ __device__ __forceinline__ float wave_sum(float v) {
 // One 256-thread workgroup per row.  VEC: 16-B loads of 16 / sizeof(elem)
 // elements (host-checked alignment, K a multiple of the vector width); the
 // second pass re-reads x from L1/L2 (8 KiB per fp16 Llama-3-8B row).
-template <int DT, bool VEC>
-__global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, int K, long long ldx,
-                                                 const void *__restrict__ w, float eps, void *__restrict__ y,
-                                                 long long ldy) {
+// ADD (LlamaDecoderLayer.forward:317-321, `residual + h` then the norm): the
+// normalised value is h' = round(x + r), written to `sum` as the new residual;
+// both passes recompute h' from x and r (same rounding, no read-after-write).
+template <int DT, bool VEC, bool ADD>
+__global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, const void *__restrict__ r, int K,
+                                                 long long ldx, const void *__restrict__ w, float eps,
+                                                 void *__restrict__ y, void *__restrict__ sum, long long ldy) {
   constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
   constexpr int V = VEC ? 16 / ES : 1;
   __shared__ float s_part[4];
   const long long row = blockIdx.x;
   const char *xr = reinterpret_cast<const char *>(x) + row * ldx * ES;
+  const char *rr = ADD ? reinterpret_cast<const char *>(r) + row * ldx * ES : nullptr;
   char *yr = reinterpret_cast<char *>(y) + row * ldy * ES;
+  char *sr = ADD ? reinterpret_cast<char *>(sum) + row * ldy * ES : nullptr;
   const int nv = K / V;
+  auto value = [&](long long e) {
+    if constexpr (ADD) return round_dt<DT>(__fadd_rn(load_f32<DT>(rr, e), load_f32<DT>(xr, e)));
+    else return load_f32<DT>(xr, e);
+  };
 
   float ss = 0.0f;
   for (int i = threadIdx.x; i < nv; i += 256) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float h = load_f32<DT>(xr, (long long)i * V + j);
+      const float h = value((long long)i * V + j);
       ss = __fadd_rn(ss, __fmul_rn(h, h));
     }
   }
@@ -58,13 +68,15 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, int
   __syncthreads();
   const float tot = __fadd_rn(__fadd_rn(s_part[0], s_part[1]), __fadd_rn(s_part[2], s_part[3]));
   // torch MeanOps: sum * (1/N) in fp32; then rsqrt(var + eps)
-  const float r = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)K), eps));
+  const float rs = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)K), eps));
   for (int i = threadIdx.x; i < nv; i += 256) {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const long long e = (long long)i * V + j;
-      const float h = round_dt<DT>(__fmul_rn(load_f32<DT>(xr, e), r));  // hidden.to(input_dtype)
-      store_f32<DT>(yr, e, __fmul_rn(load_f32<DT>(w, e), h));         // weight * hidden
+      const float v = value(e);
+      if constexpr (ADD) store_f32<DT>(sr, e, v);                     // the new residual stream
+      const float h = round_dt<DT>(__fmul_rn(v, rs));                  // hidden.to(input_dtype)
+      store_f32<DT>(yr, e, __fmul_rn(load_f32<DT>(w, e), h));          // weight * hidden
     }
   }
 }
@@ -118,11 +130,38 @@ __global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, co
   store_f32<DT>(y, i, __fmul_rn(a, load_f32<DT>(u, i)));
 }
 
-template <int DT>
-void launch_rmsnorm(bool vec, long long rows, const void *x, int K, long long ldx, const void *w, float eps, void *y,
-                    long long ldy, hipStream_t s) {
-  if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true>), dim3((unsigned)rows), dim3(256), 0, s, x, K, ldx, w, eps, y, ldy);
-  else hipLaunchKernelGGL((k_rmsnorm<DT, false>), dim3((unsigned)rows), dim3(256), 0, s, x, K, ldx, w, eps, y, ldy);
+template <int DT, bool ADD>
+void launch_rmsnorm(bool vec, long long rows, const void *x, const void *r, int K, long long ldx, const void *w,
+                    float eps, void *y, void *sum, long long ldy, hipStream_t s) {
+  const dim3 g((unsigned)rows), b(256);
+  if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
+  else hipLaunchKernelGGL((k_rmsnorm<DT, false, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
+}
+
+int rmsnorm_entry(const void *x, const void *r, int dtype, long long rows, int K, long long ldx, const void *weight,
+                  float eps, void *y, void *sum, long long ldy, void *stream) {
+  if (rows < 0 || K < 0) return QZ_ERR_ARG;
+  if (rows == 0 || K == 0) return 0;
+  if (!x || !weight || !y || ldx < K || ldy < K) return QZ_ERR_ARG;
+  if ((r != nullptr) != (sum != nullptr)) return QZ_ERR_ARG;
+  if (rows > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  const int es = dtype == QZ_DT_F32 ? 4 : 2;
+  const int v = 16 / es;
+  const bool vec = K % v == 0 && ldx % v == 0 && ldy % v == 0 &&
+                   ((uintptr_t)x | (uintptr_t)y | (uintptr_t)weight | (uintptr_t)r | (uintptr_t)sum) % 16 == 0;
+  hipStream_t s = (hipStream_t)stream;
+  const bool add = r != nullptr;
+#define QZ_NORM(DT_)                                                                       \
+  (add ? launch_rmsnorm<DT_, true>(vec, rows, x, r, K, ldx, weight, eps, y, sum, ldy, s) \
+       : launch_rmsnorm<DT_, false>(vec, rows, x, r, K, ldx, weight, eps, y, sum, ldy, s))
+  switch (dtype) {
+    case QZ_DT_F16: QZ_NORM(QZ_DT_F16); break;
+    case QZ_DT_BF16: QZ_NORM(QZ_DT_BF16); break;
+    case QZ_DT_F32: QZ_NORM(QZ_DT_F32); break;
+    default: return QZ_ERR_DTYPE;
+  }
+#undef QZ_NORM
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -132,21 +171,13 @@ using namespace qz;
 
 extern "C" int qz_rmsnorm(const void *x, int dtype, long long rows, int K, long long ldx, const void *weight,
                           float eps, void *y, long long ldy, void *stream) {
-  if (rows < 0 || K < 0) return QZ_ERR_ARG;
-  if (rows == 0 || K == 0) return 0;
-  if (!x || !weight || !y || ldx < K || ldy < K) return QZ_ERR_ARG;
-  if (rows > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
-  const int es = dtype == QZ_DT_F32 ? 4 : 2;
-  const int v = 16 / es;
-  const bool vec = K % v == 0 && ldx % v == 0 && ldy % v == 0 && ((uintptr_t)x | (uintptr_t)y | (uintptr_t)weight) % 16 == 0;
-  hipStream_t s = (hipStream_t)stream;
-  switch (dtype) {
-    case QZ_DT_F16: launch_rmsnorm<QZ_DT_F16>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
-    case QZ_DT_BF16: launch_rmsnorm<QZ_DT_BF16>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
-    case QZ_DT_F32: launch_rmsnorm<QZ_DT_F32>(vec, rows, x, K, ldx, weight, eps, y, ldy, s); break;
-    default: return QZ_ERR_DTYPE;
-  }
-  return (int)hipGetLastError();
+  return rmsnorm_entry(x, nullptr, dtype, rows, K, ldx, weight, eps, y, nullptr, ldy, stream);
+}
+
+extern "C" int qz_add_rmsnorm(const void *x, const void *residual, int dtype, long long rows, int K, long long ldx,
+                              const void *weight, float eps, void *sum, void *y, long long ldy, void *stream) {
+  if (!residual || !sum) return QZ_ERR_ARG;
+  return rmsnorm_entry(x, residual, dtype, rows, K, ldx, weight, eps, y, sum, ldy, stream);
 }
 
 extern "C" int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long long *q_str, void *q_out,

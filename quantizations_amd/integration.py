@@ -131,6 +131,8 @@ def unfuse_projection_groups(model: nn.Module) -> None:
 RMSNORM_CLASSES = ("LlamaRMSNorm", "MistralRMSNorm", "Qwen2RMSNorm")
 # MLPs whose forward is down_proj(act_fn(gate_proj(x)) * up_proj(x)) (modeling_llama.py:174-176)
 MLP_CLASSES = ("LlamaMLP", "MistralMLP", "Qwen2MLP")
+# decoder layers whose forward is exactly LlamaDecoderLayer's (modeling_llama.py:295-324)
+DECODER_CLASSES = ("LlamaDecoderLayer",)
 _ROPE_PATCHED = {}  # module name -> original apply_rotary_pos_emb
 
 
@@ -166,13 +168,41 @@ def _fused_mlp_forward(mod: nn.Module):
     return forward
 
 
-def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True) -> int:
+def _fused_decoder_forward(mod: nn.Module):
+    """LlamaDecoderLayer.forward (modeling_llama.py:295-324) with lines 317-321
+    (`residual + h`, then post_attention_layernorm) as one add_rms_norm launch."""
+    from .layer_ops import add_rms_norm, add_rms_norm_supported
+
+    def forward(hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
+                position_embeddings=None, **kwargs):
+        residual = hidden_states
+        h = mod.input_layernorm(hidden_states)
+        h, _ = mod.self_attn(hidden_states=h, attention_mask=attention_mask, position_ids=position_ids,
+                             past_key_values=past_key_values, use_cache=use_cache,
+                             position_embeddings=position_embeddings, **kwargs)
+        ln = mod.post_attention_layernorm
+        if add_rms_norm_supported(h, residual, ln.weight):
+            residual, h = add_rms_norm(h, residual, ln.weight, ln.variance_epsilon)
+        else:
+            h = residual + h
+            residual = h
+            h = ln(h)
+        h = mod.mlp(h)
+        return residual + h
+    return forward
+
+
+def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
+                   decoder: bool = False) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
-    attention modules and the SiLU-gate product of its MLPs through one HIP
-    launch each (layer_ops.rms_norm / rope_qk / silu_mul) instead of
-    transformers' 8-, 10- and 2-launch eager forms.  Inputs the kernels do not
+    attention modules, the SiLU-gate product of its MLPs and each decoder
+    layer's residual add + post-attention norm through one HIP launch each
+    (layer_ops.rms_norm / rope_qk / silu_mul / add_rms_norm) instead of
+    transformers' 8-, 10-, 2- and 9-launch eager forms.  Inputs the kernels do not
     take keep the original code.  Returns the number of modules patched (norms,
-    MLPs, and modeling modules whose apply_rotary_pos_emb was replaced)."""
+    MLPs, decoder layers, and modeling modules whose apply_rotary_pos_emb was
+    replaced).  `decoder` (opt-in) replaces LlamaDecoderLayer.forward itself with
+    a restatement; it measured no gain on the bs=1 graph step."""
     import sys
 
     n = 0
@@ -181,6 +211,12 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
         if norm and name in RMSNORM_CLASSES and "forward" not in m.__dict__ and hasattr(m, "variance_epsilon"):
             m.__dict__["forward"] = _fused_rmsnorm_forward(m, m.forward)
             m.__dict__["_qz_fused_norm"] = True
+            n += 1
+        elif decoder and name in DECODER_CLASSES and "forward" not in m.__dict__ and \
+                type(getattr(m, "post_attention_layernorm", None)).__name__ in RMSNORM_CLASSES and \
+                all(hasattr(m, a) for a in ("input_layernorm", "self_attn", "mlp")):
+            m.__dict__["forward"] = _fused_decoder_forward(m)
+            m.__dict__["_qz_fused_decoder"] = True
             n += 1
         elif mlp and name in MLP_CLASSES and "forward" not in m.__dict__ and \
                 "silu" in type(getattr(m, "act_fn", None)).__name__.lower() and \
@@ -204,7 +240,8 @@ def unfuse_layer_ops(model: nn.Module) -> None:
     import sys
 
     for m in model.modules():
-        if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None):
+        if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None) or \
+                m.__dict__.pop("_qz_fused_decoder", None):
             m.__dict__.pop("forward", None)
     for modname, fn in list(_ROPE_PATCHED.items()):
         setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)

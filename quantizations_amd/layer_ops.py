@@ -6,7 +6,9 @@ projections (csrc/layer_ops.hip, C-ABI include/quantizations.h):
 * ``rope_qk``   -- apply_rotary_pos_emb (modeling_llama.py:138-160), applied to
   the outputs of q_proj/k_proj;
 * ``silu_mul``  -- LlamaMLP's act_fn(gate_proj(x)) * up_proj(x)
-  (modeling_llama.py:175), the input of down_proj.
+  (modeling_llama.py:175), the input of down_proj;
+* ``add_rms_norm`` -- LlamaDecoderLayer's ``residual + h`` followed by the
+  post-attention RMSNorm (modeling_llama.py:317-321).
 
 None of them is in the reference (it leaves them to transformers).  They exist
 because at batch-1 decode the eager torch forms cost ~8, ~10 and 2 dependent
@@ -44,6 +46,26 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
                                    weight.data_ptr(), float(eps), y.data_ptr(), K, _lib.stream_of(x)),
                "qz_rmsnorm")
     return y
+
+
+def add_rms_norm_supported(x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (rms_norm_supported(x, weight) and residual.dtype == x.dtype and residual.device == x.device
+            and residual.shape == x.shape and x.is_contiguous() and residual.is_contiguous())
+
+
+def add_rms_norm(x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor, eps: float):
+    """(s, rms_norm(s)) with s = residual + x (rounded to x.dtype, bit-exact to the
+    torch add), one launch."""
+    if not add_rms_norm_supported(x, residual, weight):
+        raise ValueError("add_rms_norm: unsupported input")
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    s = torch.empty_like(x)
+    y = torch.empty_like(x)
+    _lib.check(_lib.lib.qz_add_rmsnorm(x.data_ptr(), residual.data_ptr(), _lib.dtype_code(x.dtype), rows, K, K,
+                                       weight.data_ptr(), float(eps), s.data_ptr(), y.data_ptr(), K,
+                                       _lib.stream_of(x)), "qz_add_rmsnorm")
+    return s, y
 
 
 def _strides3(t: torch.Tensor):

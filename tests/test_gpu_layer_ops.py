@@ -10,6 +10,7 @@ Bars:
     LlamaRMSNorm.forward -- a 1-ulp change of the rounded normalised value,
     times the weight, rounded again -- and >= 99 % of elements bit-identical
     (fp16/bf16); fp32 outputs within 4 ulp.
+  * add_rms_norm: the residual sum bit-exact, the norm as rms_norm.
   * silu_mul: vs F.silu(g) * u, >= 99 % bit-identical, all within 2 ulp
     (torch's and the kernel's expf may differ in the last place).
   * tiny Llama with fuse_layer_ops: greedy tokens identical to the unfused
@@ -115,6 +116,25 @@ def test_silu_mul_vs_torch(dtype, shape):
     assert (y == ref).float().mean().item() >= 0.99
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("shape", [(1, 1, 4096), (4, 1, 4096), (2, 9, 1000)])
+def test_add_rms_norm_vs_residual_add_and_llama_rmsnorm(dtype, shape):
+    from quantizations_amd.layer_ops import add_rms_norm
+
+    K = shape[-1]
+    m = _hf_norm(K, dtype)
+    x = (torch.randn(shape, device=DEV) * 3).to(dtype)
+    r = (torch.randn(shape, device=DEV) * 3).to(dtype)
+    with torch.no_grad():
+        s_ref = r + x
+        y_ref = m(s_ref)
+        s, y = add_rms_norm(x, r, m.weight, m.variance_epsilon)
+    assert torch.equal(s, s_ref)  # the residual stream is bit-exact
+    d = (y.double() - y_ref.double()).abs()
+    ulps = 4 if dtype == torch.float32 else 2
+    assert bool((d <= ulps * _ulp_at(y_ref, dtype)).all()), float(d.max())
+
+
 def _tiny_llama(seed=3):
     from transformers import LlamaConfig, LlamaForCausalLM
 
@@ -175,8 +195,8 @@ def test_tiny_llama_fuse_layer_ops_decode_and_graph():
     with torch.no_grad():
         ref_toks, ref_logits = greedy(6)
         ref_graph = graph_logits(ref_toks[:, :1])
-        n = fuse_layer_ops(model)
-        assert n == 3 * cfg.num_hidden_layers + 1 + 1  # 2 norms + 1 MLP per layer, final norm, one modeling module
+        n = fuse_layer_ops(model, decoder=True)
+        assert n == 4 * cfg.num_hidden_layers + 1 + 1  # 2 norms + MLP + decoder layer each, final norm, rope
         toks, logits = greedy(6)
         assert torch.equal(toks, ref_toks)
         for a, b in zip(logits, ref_logits):

@@ -111,7 +111,7 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     orig = ml.apply_rotary_pos_emb
     with torch.no_grad():
         ref = model(input_ids=ids).logits
-        assert fuse_layer_ops(model) == 2 * 2 + 1 + 2 + 1  # norms, final norm, MLPs, one modeling module
+        assert fuse_layer_ops(model, decoder=True) == 2 * 2 + 1 + 2 + 2 + 1  # norms, final norm, MLPs, decoder layers, rope
         assert ml.apply_rotary_pos_emb is not orig and ml.apply_rotary_pos_emb._qz_orig is orig
         assert fuse_layer_ops(model) == 0  # idempotent
         assert torch.equal(model(input_ids=ids).logits, ref)

@@ -69,3 +69,8 @@ def test_argument_errors_are_reported_not_launched():
     s2 = (ctypes.c_longlong * 2)(0, 0)
     assert L.qz_rope_qk(0, 1, 1, 127, 1, 1, s3, 1, s3, 1, 1, s3, 1, s3, 1, 1, s2, 0) == -3
     assert L.qz_rope_qk(0, 1, 1, 128, 1, 1, s3, 1, s3, 1, 1, s3, 1, s3, 0, 1, s2, 0) == -1
+    assert L.qz_silu_mul(1, 1, 0, -1, 1, 0) == -1
+    assert L.qz_silu_mul(0, 1, 0, 16, 1, 0) == -1
+    assert L.qz_silu_mul(1, 1, 9, 16, 1, 0) == -4
+    assert L.qz_add_rmsnorm(1, 0, 0, 4, 64, 64, 1, 1e-6, 1, 1, 64, 0) == -1  # residual required
+    assert L.qz_add_rmsnorm(1, 1, 0, 4, 64, 64, 1, 1e-6, 0, 1, 64, 0) == -1  # sum output required

@@ -524,18 +524,18 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 // zero row.  TB = 0: the direct fragment loads (kept for the microbenchmark).
 constexpr int kMtChunk = 256, kMtWaves = 8;
 constexpr int kMtXRow = kMtChunk * 2 + 16;  // padded LDS row of one token's chunk of X
-template <int QT, bool DQ, int DT, int TB = 0>
+template <int QT, bool DQ, int DT, int TB = 0, int W = kMtWaves>
 __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
   constexpr int XL = TB > 0 ? (TB + 1) / 2 : 1;  // staging loads per lane per chunk (two token rows each)
   __shared__ float s_code2[DQ ? 256 : 1];
-  __shared__ f4_t s_red[kMtWaves][64];
-  __shared__ __attribute__((aligned(16))) unsigned char s_xs[TB > 0 ? kMtWaves * (TB + 1) * kMtXRow : 16];
+  __shared__ f4_t s_red[W][64];
+  __shared__ __attribute__((aligned(16))) unsigned char s_xs[TB > 0 ? W * (TB + 1) * kMtXRow : 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int m0 = block * 16;
   const int nch = p.K / kMtChunk;
-  const int ch0 = wave * nch / kMtWaves, ch1 = (wave + 1) * nch / kMtWaves;
+  const int ch0 = wave * nch / W, ch1 = (wave + 1) * nch / W;
   const int wrow = min(m0 + r, p.M - 1);
   const uint32_t row_bytes = (uint32_t)p.K >> 1;
   const unsigned char *wptr = p.B + (size_t)wrow * row_bytes + 32 * g;
@@ -645,16 +645,16 @@ __device__ __forceinline__ void mt_body(const GemmParams &p, const int block) {
     if (c < p.T && m < p.M) {
       float v = 0.0f;
 #pragma unroll
-      for (int w = 0; w < kMtWaves; ++w) v += s_red[w][l][i];
+      for (int w = 0; w < W; ++w) v += s_red[w][l][i];
       if (p.bias) v += load_f32<DT>(p.bias, m);
       store_f32<DT>(p.Y, (long long)c * p.ldy + m, v);
     }
   }
 }
 
-template <int QT, bool DQ, int DT, int TB>
-__global__ __launch_bounds__(64 * kMtWaves) void k_gemv_4bit_mt(GemmParams p) {
-  mt_body<QT, DQ, DT, TB>(p, blockIdx.x);
+template <int QT, bool DQ, int DT, int TB, int W = kMtWaves>
+__global__ __launch_bounds__(64 * W) void k_gemv_4bit_mt(GemmParams p) {
+  mt_body<QT, DQ, DT, TB, W>(p, blockIdx.x);
 }
 
 // token bucket of the staged multi-token kernel: LDS image rows per wave

@@ -49,7 +49,16 @@ int main(int argc, char **argv) {
 #define MT(T_, TB_) vs.push_back({"mt T=" #T_ " TB=" #TB_, [&, pt = p](int i) { GemmParams q = pt; q.T = T_; \
     q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
     hipLaunchKernelGGL((k_gemv_4bit_mt<QZ_NF4, true, QZ_DT_F16, TB_>), dim3(grid), dim3(512), 0, 0, q); }, {}})
-  MT(2, 0); MT(2, 2); MT(4, 0); MT(4, 4); MT(8, 0); MT(8, 8); MT(16, 0); MT(16, 16); MT(3, 4); MT(5, 8);
+  const bool waves = argc > 3 && std::string(argv[3]) == "waves";
+  // waves-per-workgroup variants (K split W ways inside the workgroup; W = 8 is the product)
+#define MTW(T_, TB_, W_) vs.push_back({"mt T=" #T_ " TB=" #TB_ " W=" #W_, [&, pt = p](int i) { GemmParams q = pt; q.T = T_; \
+    q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    hipLaunchKernelGGL((k_gemv_4bit_mt<QZ_NF4, true, QZ_DT_F16, TB_, W_>), dim3(grid), dim3(64 * W_), 0, 0, q); }, {}})
+  if (waves) {
+    MTW(2, 2, 4); MTW(2, 2, 8); MTW(2, 2, 16); MTW(8, 8, 4); MTW(8, 8, 8); MTW(8, 8, 16);
+  } else {
+    MT(2, 0); MT(2, 2); MT(4, 0); MT(4, 4); MT(8, 0); MT(8, 8); MT(16, 0); MT(16, 16); MT(3, 4); MT(5, 8);
+  }
   for (auto &v : vs) for (int i = 0; i < NC; ++i) v.f(i);
   CK(hipDeviceSynchronize());
   for (int r = 0; r < ROUNDS; ++r)

@@ -11,16 +11,16 @@ config #1 CPU dequant+matmul baseline.
   fp16 (transformers' default skip list).  A step = one generated token
   (full forward: embeddings, 32 layers with attention + KV cache, lm_head,
   argmax).  value = generated tokens / s.
-* N > 1 (torchrun, one process per GPU), default --tp-mode pair: Megatron
-  pairing -- q/k/v and gate/up column-parallel (rank p keeps its heads / MLP
-  columns as row slices of the global quant state), o_proj and down_proj
-  row-parallel (input-column slices) + one RCCL all-reduce each: 2 collectives
-  per layer.  --tp-mode gather: every Linear4bit row-split + all-gather.
-  Weak scaling (default): each GPU adds one bs=1 decode stream (global batch
-  N) and every layer is sharded over all N GPUs, so each GPU streams 1/N of
-  the weights once per step for N tokens -- per-GPU work fixed.  --strong:
-  one bs=1 stream served by all N GPUs (config #5's literal layout; latency-
-  bound on the collectives at bs=1).
+* N > 1 (torchrun, one process per GPU), default: the north-star layout
+   -- ONE bs=1 decode stream served by all N GPUs,
+  every Linear4bit row-split (rank p keeps rows [p*M/N, (p+1)*M/N) of the
+  global quant state) and its fp16 output RCCL all-gathered over xGMI
+  (q/k/v and gate/up shards exchanged by one all-gather per group): strong
+  scaling, global batch 1, parallelism tp{N}-rowsplit-allgather.  The
+  weak-scaling layout (--weak: one bs=1 stream per GPU, global batch N,
+  Megatron pairing -- q/k/v/gate/up column-parallel, o/down row-parallel +
+  one all-reduce each) is measured after it and reported only as the extra
+  key `weak_scaling_extra` (--no-extra-weak skips it).
 * roofline: the 4096x4096 NF4+DQ fused GEMV alone, 64 rotating weight copies
   (> the 256 MiB Infinity Cache), HIP events on the launch stream around 400
   back-to-back launches (average launch duration, matches rocprofv3);
@@ -115,14 +115,19 @@ def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: in
 
 
 @torch.inference_mode()
-def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int, batch: int = 1):
+def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int, batch: int = 1,
+                       graph: bool = True, device: str = "cuda"):
     """Same workload as decode_bench, with the decode step captured once into a HIP
     graph (StaticCache, static token/position buffers; the graph contains the
     whole forward, the argmax and the feedback of the token into the next
-    step).  One replay = one generated token per stream (`batch` streams)."""
+    step).  One replay = one generated token per stream (`batch` streams).
+    graph=False runs the identical step eagerly (the gloo CPU test of the
+    multi-GPU layout drives this function with it).  Returns (seconds for the
+    timed steps, token history [batch, prompt + warmup + steps + 8])."""
     from transformers.cache_utils import StaticCache
 
-    dev = torch.device("cuda")
+    dev = torch.device(device)
+    cuda = dev.type == "cuda"
     g = torch.Generator(device="cpu").manual_seed(1234)
     ids = torch.randint(0, cfg.vocab_size, (batch, prompt_len), generator=g).to(dev)
     cache = StaticCache(config=cfg, max_cache_len=prompt_len + warmup + steps + 8)
@@ -141,28 +146,65 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
         tok.copy_(nxt)
         pos.add_(1)
 
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(2):
+    run = step
+    if graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg, capture_error_mode=CAPTURE_MODE):
             step()
-    torch.cuda.current_stream().wait_stream(s)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
-        step()
+        run = cg.replay
     for _ in range(warmup):
-        graph.replay()
+        run()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if cuda:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        graph.replay()
-    torch.cuda.synchronize()
+        run()
+    if cuda:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     return dt, hist
+
+
+def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
+                         fuse: bool = True, layer_ops: str = "all", local_matmul=None):
+    """The bench's model layout after replace_with_bnb_linear: shard every
+    Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
+    "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
+    groups and the one-launch layer ops.  `local_matmul` is the CPU test hook of
+    parallel.py (None = the HIP kernels).  Returns (n_groups, n_layer_ops)."""
+    if sharded:
+        if tp_mode == "pair":
+            from quantizations_amd.parallel import apply_tensor_parallel
+            apply_tensor_parallel(model, rank, world, local_matmul=local_matmul)
+        else:
+            from quantizations_amd.parallel import shard_model_linear4bit
+            shard_model_linear4bit(model, rank, world, local_matmul=local_matmul)
+        import gc
+        gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    n_groups = 0
+    if fuse:
+        from quantizations_amd.integration import fuse_projection_groups
+        n_groups = fuse_projection_groups(model)   # q/k/v and gate/up: one grouped GEMV launch each
+    n_layer_ops = 0
+    if layer_ops != "none":
+        from quantizations_amd.integration import fuse_layer_ops
+        n_layer_ops = fuse_layer_ops(model, norm=layer_ops in ("all", "all+decoder", "norm"),
+                                     rope=layer_ops in ("all", "all+decoder", "rope"),
+                                     mlp=layer_ops in ("all", "all+decoder", "mlp"),
+                                     decoder=layer_ops == "all+decoder")  # one HIP launch each
+    return n_groups, n_layer_ops
 
 
 @torch.inference_mode()
@@ -444,18 +486,25 @@ def main():
     ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
                     help="torch.cuda.graph capture_error_mode of the decode-step capture")
     ap.add_argument("--prefill-sweep", action="store_true", help="fused vs dequant+hipBLASLt over T (4096x4096)")
-    ap.add_argument("--tp-mode", choices=("pair", "gather"), default="pair",
-                    help="multi-GPU layout: Megatron pairing (column q/k/v/gate/up + row o/down, 2 all-reduces per "
-                         "layer) or row-split every Linear4bit + all-gather")
+    ap.add_argument("--tp-mode", choices=("pair", "gather"), default=None,
+                    help="multi-GPU layout: row-split every Linear4bit + all-gather (default; the north-star "
+                         "layout) or Megatron pairing (column q/k/v/gate/up + row o/down, 2 all-reduces per "
+                         "layer; the --weak default)")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the multi-GPU code path (process group, sharded layers, RCCL) even at world size 1")
     ap.add_argument("--batch", type=int, default=1,
-                    help="decode streams per GPU (bs=1 each); the global batch is batch x N (weak scaling)")
-    ap.add_argument("--strong", action="store_true",
-                    help="N > 1: keep the global batch at --batch (one bs=1 stream served by all N GPUs)")
+                    help="decode streams (bs=1 each); with --weak the global batch is batch x N")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: weak scaling -- one bs=1 stream per GPU (global batch = batch x N), Megatron "
+                         "pairing unless --tp-mode says otherwise")
+    ap.add_argument("--strong", action="store_true", help="(default) N > 1: the global batch stays --batch")
+    ap.add_argument("--no-extra-weak", action="store_true",
+                    help="N > 1: skip the extra weak-scaling (TP-pair, global batch N) measurement")
     args = ap.parse_args()
     global CAPTURE_MODE
     CAPTURE_MODE = args.capture_mode
+    if args.weak and args.strong:
+        ap.error("--weak and --strong are exclusive")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -481,57 +530,60 @@ def main():
         print(json.dumps(prefill_sweep()), flush=True)
         return
 
-    t_build = time.perf_counter()
-    model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
-                             double_quant=not args.no_dq)
-    if sharded:
-        if args.tp_mode == "pair":
-            from quantizations_amd.parallel import apply_tensor_parallel
-            apply_tensor_parallel(model, rank, world)
-        else:
-            from quantizations_amd.parallel import shard_model_linear4bit
-            shard_model_linear4bit(model, rank, world)
-        import gc
-        gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
-        torch.cuda.empty_cache()
-    n_groups = 0
-    if not args.no_fuse:
-        from quantizations_amd.integration import fuse_projection_groups
-        n_groups = fuse_projection_groups(model)   # q/k/v and gate/up: one grouped GEMV launch each
-    n_layer_ops = 0
-    if not args.no_layer_ops and args.layer_ops != "none":
-        from quantizations_amd.integration import fuse_layer_ops
-        n_layer_ops = fuse_layer_ops(model, norm=args.layer_ops in ("all", "all+decoder", "norm"),
-                                     rope=args.layer_ops in ("all", "all+decoder", "rope"),
-                                     mlp=args.layer_ops in ("all", "all+decoder", "mlp"),
-                                     decoder=args.layer_ops == "all+decoder")  # one HIP launch each
-    log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
-        f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB")
+    layer_ops = "none" if args.no_layer_ops else args.layer_ops
 
-    # Weak scaling (default): every GPU adds one bs=1 decode stream and every
-    # Linear4bit is sharded over all N GPUs (TP), so per-GPU work -- weight bytes
-    # x tokens -- stays fixed as N grows.  --strong: one global batch for any N.
-    gbatch = args.batch if (args.strong or not sharded) else args.batch * world
-    mode = "eager"
-    if not args.eager:
-        try:
-            dt, toks = decode_bench_graph(model, cfg, args.steps, args.warmup, args.prompt, world, gbatch)
-            mode = "hipgraph"
-        except Exception as e:  # capture unsupported by this transformers build -> eager
-            log(f"[rank {rank}] graph decode failed ({type(e).__name__}: {e}); falling back to eager")
-            torch.cuda.synchronize()
-    if mode == "eager":
-        dt, toks = decode_bench(model, cfg, args.steps, args.warmup, args.prompt, world, gbatch)
-    t = torch.tensor([dt], device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int):
+        t_build = time.perf_counter()
+        model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
+                                 double_quant=not args.no_dq)
+        n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
+                                                     layer_ops=layer_ops)
+        log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
+            f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
+        mode = "eager"
+        if not args.eager:
+            try:
+                dt, _ = decode_bench_graph(model, cfg, steps, warmup, args.prompt, world, gbatch)
+                mode = "hipgraph"
+            except Exception as e:  # capture unsupported by this transformers build -> eager
+                log(f"[rank {rank}] graph decode failed ({type(e).__name__}: {e}); falling back to eager")
+                torch.cuda.synchronize()
+        if mode == "eager":
+            dt, _ = decode_bench(model, cfg, steps, warmup, args.prompt, world, gbatch)
+        t = torch.tensor([dt], device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time
+        del model
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        return float(t.item()), mode, cfg, n_groups, n_layer_ops
+
+    def parallelism(tp_mode: str) -> str:
+        if not sharded:
+            return "single"
+        return f"tp{world}-megatron-pair-allreduce" if tp_mode == "pair" else f"tp{world}-rowsplit-allgather"
+
+    # Strong scaling (default): ONE global batch (bs=1) for any N, every Linear4bit
+    # row-split over all N GPUs + all-gather.  --weak: every GPU adds one bs=1
+    # stream (global batch batch x N) and the layers are TP-paired.
+    weak = args.weak and sharded
+    tp_mode = args.tp_mode or ("pair" if weak else "gather")
+    gbatch = args.batch * world if weak else args.batch
+    dt, mode, cfg, n_groups, n_layer_ops = run_decode(tp_mode, gbatch, args.steps, args.warmup)
     tok_s = args.steps * gbatch / dt   # tokens generated by all streams, whole job
+
+    extra_weak = None
+    if world > 1 and not weak and not args.no_extra_weak:
+        # the weak-scaling layout, reported beside the headline only (extra key)
+        w_steps = max(8, args.steps // 2)
+        wdt, wmode, _, _, _ = run_decode("pair", args.batch * world, w_steps, args.warmup)
+        extra_weak = {"value": round(w_steps * args.batch * world / wdt, 3), "unit": "tokens/s",
+                      "ms_per_step": round(wdt / w_steps * 1e3, 4), "steps": w_steps, "scaling": "weak",
+                      "global_batch": args.batch * world, "decode": wmode, "parallelism": parallelism("pair")}
 
     roof = None
     if rank == 0 and not args.no_roofline:
-        del model
-        torch.cuda.empty_cache()
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         # average launch duration = HIP events around `iters` back-to-back launches on
         # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
@@ -569,18 +621,18 @@ def main():
             "metric": "decode tokens/sec Llama-3-8B NF4 bs=1; 4096×4096 GEMV GB/s vs HBM peak",
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
+            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
             "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}-decode-bs1",
                        "layers": cfg.num_hidden_layers,
                        "prompt_len": args.prompt, "global_batch": gbatch, "streams_per_gpu": gbatch / world,
                        "stream_batch": 1, "decode": mode,
-                       "parallelism": ("single" if not sharded else
-                                       f"tp{world}-megatron-pair-allreduce" if args.tp_mode == "pair" else
-                                       f"tp{world}-rowsplit-allgather"),
+                       "parallelism": parallelism(tp_mode),
                        "projection_groups": n_groups, "layer_ops": n_layer_ops},
             "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
+        if extra_weak is not None:
+            line["weak_scaling_extra"] = extra_weak
         print(json.dumps(line), flush=True)
     if sharded:
         dist.barrier()

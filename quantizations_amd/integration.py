@@ -133,6 +133,10 @@ RMSNORM_CLASSES = ("LlamaRMSNorm", "MistralRMSNorm", "Qwen2RMSNorm")
 MLP_CLASSES = ("LlamaMLP", "MistralMLP", "Qwen2MLP")
 # decoder layers whose forward is exactly LlamaDecoderLayer's (modeling_llama.py:295-324)
 DECODER_CLASSES = ("LlamaDecoderLayer",)
+# attention modules whose modeling module's apply_rotary_pos_emb is Llama's half-split
+# rotation (modeling_llama.py:138-160); others (e.g. Cohere's interleaved
+# rotate_half) keep their own code
+ATTENTION_CLASSES = ("LlamaAttention", "MistralAttention", "Qwen2Attention")
 _ROPE_PATCHED = {}  # module name -> original apply_rotary_pos_emb
 
 
@@ -144,6 +148,19 @@ def _fused_rmsnorm_forward(mod: nn.Module, orig):
             return rms_norm(hidden_states, mod.weight, mod.variance_epsilon)
         return orig(hidden_states)  # transformers' own eager code (e.g. CPU tensors, mixed dtypes)
     return forward
+
+
+def _half_split_rotate(mod) -> bool:
+    """True iff the modeling module's rotate_half is the half-split form
+    cat(-x[..., D/2:], x[..., :D/2]) that k_rope_qk implements."""
+    fn = getattr(mod, "rotate_half", None)
+    if fn is None:
+        return False
+    try:
+        r = fn(torch.arange(1.0, 5.0))
+    except Exception:
+        return False
+    return isinstance(r, torch.Tensor) and r.tolist() == [-3.0, -4.0, 1.0, 2.0]
 
 
 def _fused_rope(orig):
@@ -224,11 +241,11 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
             m.__dict__["forward"] = _fused_mlp_forward(m)
             m.__dict__["_qz_fused_mlp"] = True
             n += 1
-        elif rope and name.endswith("Attention"):
+        elif rope and name in ATTENTION_CLASSES:
             modname = type(m).__module__
             mod = sys.modules.get(modname)
             fn = getattr(mod, "apply_rotary_pos_emb", None)
-            if fn is not None and modname not in _ROPE_PATCHED:
+            if fn is not None and modname not in _ROPE_PATCHED and _half_split_rotate(mod):
                 _ROPE_PATCHED[modname] = fn
                 mod.apply_rotary_pos_emb = _fused_rope(fn)
                 n += 1

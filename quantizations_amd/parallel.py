@@ -237,7 +237,10 @@ def shard_cols(packed: torch.Tensor, qs: QuantState, rank: int, world: int) -> C
 class RowParallelLinear4bit(nn.Module):
     """Megatron row-parallel 4-bit layer: this rank's input columns; takes the
     LOCAL slice of the activation (the output of a column-parallel layer) and
-    all-reduces the partial products.  The bias is added once (rank 0)."""
+    all-reduces the partial products.  The bias is added once (rank 0).  The
+    partials are summed in fp32 and rounded to the activation dtype once, so the
+    result differs from the single-GPU layer only by the one rounding of each
+    rank's partial (not by P extra fp16 roundings inside the collective)."""
 
     def __init__(self, full: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
                  group=None, local_matmul: Optional[Callable] = None):
@@ -268,9 +271,9 @@ class RowParallelLinear4bit(nn.Module):
                 y = gemv_4bit(x_local, self.packed, state=self.state, bias=self.bias)
             else:
                 y = gemm_4bit(x_local, self.packed, self.state, bias=self.bias)
-        y = y.contiguous()
-        dist.all_reduce(y, group=self.group)
-        return y
+        y32 = y.float().contiguous()   # [..., M] fp32: 16 KiB at bs=1 for M = 4096
+        dist.all_reduce(y32, group=self.group)
+        return y32.to(y.dtype)
 
 
 # (column-parallel, row-parallel) projection names per block kind
@@ -310,13 +313,14 @@ def apply_tensor_parallel(model: nn.Module, rank: Optional[int] = None, world_si
 
 
 def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                           group=None) -> nn.Module:
-    """Replace every Linear4bit of `model` by its RowShardedLinear4bit."""
+                           group=None, local_matmul: Optional[Callable] = None) -> nn.Module:
+    """Replace every Linear4bit of `model` by its RowShardedLinear4bit (row split +
+    all-gather: the north-star multi-GPU layout)."""
     from .modules import Linear4bit
 
     for name, child in list(model.named_children()):
         if isinstance(child, Linear4bit):
-            model._modules[name] = RowShardedLinear4bit(child, rank, world_size, group)
+            model._modules[name] = RowShardedLinear4bit(child, rank, world_size, group, local_matmul)
         else:
-            shard_model_linear4bit(child, rank, world_size, group)
+            shard_model_linear4bit(child, rank, world_size, group, local_matmul)
     return model

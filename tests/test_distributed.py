@@ -195,46 +195,52 @@ def _tp_hook(x, mod):
     return y.to(x.dtype)
 
 
+def _tiny_llama_4bit():
+    """A tiny fp32 Llama whose decoder linears are Linear4bit layers built from
+    ORACLE-quantised weights (layer 0 NF4, layer 1 FP4, double quant), plus the
+    unsharded reference model holding the oracle's dequantised weights."""
+    import copy
+
+    import oracle
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.core import Params4bit, QuantState, create_dynamic_map, get_4bit_type
+    from quantizations_amd.modules import Linear4bit
+
+    cfg = LlamaConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=97)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).float().eval()
+    ref = copy.deepcopy(model)
+    for name, lin in list(model.named_modules()):
+        if not isinstance(lin, torch.nn.Linear) or name == "lm_head":
+            continue
+        M, K = lin.out_features, lin.in_features
+        qt = "nf4" if ".layers.0." in name else "fp4"   # one format per layer: groups need it
+        W = lin.weight.detach().half()
+        st = oracle.quantize_4bit(W.float().numpy(), 64, qt, double_quant=True)
+        qs = QuantState(absmax=torch.from_numpy(st.qabsmax), shape=torch.Size([M, K]),
+                        code=get_4bit_type(qt, "cpu"), blocksize=64, quant_type=qt, dtype=torch.float16,
+                        offset=torch.tensor(float(st.offset)),
+                        state2=QuantState(absmax=torch.from_numpy(st.absmax2), blocksize=256,
+                                          code=create_dynamic_map(), dtype=torch.float32))
+        l4 = Linear4bit(K, M, bias=False, quant_type=qt, device="meta")
+        l4.weight = Params4bit.from_prequantized(torch.from_numpy(st.packed).reshape(-1, 1),
+                                                 qs.as_dict(packed=True), device="cpu", module=l4)
+        parent = model.get_submodule(name.rsplit(".", 1)[0])
+        parent._modules[name.rsplit(".", 1)[1]] = l4
+        ref.get_submodule(name).weight.data.copy_(torch.from_numpy(oracle.dequantize(st)).reshape(M, K))
+    return cfg, model, ref
+
+
 def _tp_worker(rank, world, port, q, batch=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import copy
-
-        import oracle
-        from transformers import LlamaConfig, LlamaForCausalLM
-
-        from quantizations_amd.core import Params4bit
         from quantizations_amd.integration import fuse_projection_groups
-        from quantizations_amd.modules import Linear4bit
         from quantizations_amd.parallel import RowParallelLinear4bit, apply_tensor_parallel
 
-        cfg = LlamaConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
-                          num_key_value_heads=2, vocab_size=97)
-        torch.manual_seed(0)
-        model = LlamaForCausalLM(cfg).float().eval()
-        ref = copy.deepcopy(model)
-        seed = 0
-        for name, lin in list(model.named_modules()):
-            if not isinstance(lin, torch.nn.Linear) or name == "lm_head":
-                continue
-            seed += 1
-            M, K = lin.out_features, lin.in_features
-            qt = "nf4" if ".layers.0." in name else "fp4"   # one format per layer: groups need it
-            W = lin.weight.detach().half()
-            st = oracle.quantize_4bit(W.float().numpy(), 64, qt, double_quant=True)
-            from quantizations_amd.core import QuantState, create_dynamic_map, get_4bit_type
-            qs = QuantState(absmax=torch.from_numpy(st.qabsmax), shape=torch.Size([M, K]),
-                            code=get_4bit_type(qt, "cpu"), blocksize=64, quant_type=qt, dtype=torch.float16,
-                            offset=torch.tensor(float(st.offset)),
-                            state2=QuantState(absmax=torch.from_numpy(st.absmax2), blocksize=256,
-                                              code=create_dynamic_map(), dtype=torch.float32))
-            l4 = Linear4bit(K, M, bias=False, quant_type=qt, device="meta")
-            l4.weight = Params4bit.from_prequantized(torch.from_numpy(st.packed).reshape(-1, 1),
-                                                     qs.as_dict(packed=True), device="cpu", module=l4)
-            parent = model.get_submodule(name.rsplit(".", 1)[0])
-            parent._modules[name.rsplit(".", 1)[1]] = l4
-            ref.get_submodule(name).weight.data.copy_(torch.from_numpy(oracle.dequantize(st)).reshape(M, K))
+        cfg, model, ref = _tiny_llama_4bit()
         n = apply_tensor_parallel(model, rank, world, local_matmul=_tp_hook)
         groups = fuse_projection_groups(model)
         ids = torch.tensor([[5, 17, 3, 88, 41, 9], [7, 2, 60, 11, 4, 30]])[:batch]
@@ -287,3 +293,124 @@ def test_tensor_parallel_pairing_tiny_llama(batch):
         assert n == 4 and groups == 4 and is_rowpar, (rank, n, groups)
         assert qshape == 128 * 64 // 2   # q_proj rows 64 of 128 on each rank
         assert rel < 1e-5 and rel_step < 1e-5, (rank, rel, rel_step)
+
+
+def _bench_layout_worker(rank, world, port, q, tp_mode, batch):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from quantizations_amd.parallel import RowShardedLinear4bit
+
+        cfg, model, ref = _tiny_llama_4bit()
+        n_groups, _ = bench.prepare_decode_model(model, rank, world, True, tp_mode, fuse=True, layer_ops="none",
+                                                 local_matmul=_tp_hook)
+        # bench.py's own decode loop (StaticCache, static token/position buffers, token
+        # feedback), eagerly on CPU; the reference is the unsharded dequantised model
+        _, hist = bench.decode_bench_graph(model, cfg, steps=5, warmup=2, prompt_len=6, world=world, batch=batch,
+                                           graph=False, device="cpu")
+        _, ref_hist = bench.decode_bench_graph(ref, cfg, steps=5, warmup=2, prompt_len=6, world=1, batch=batch,
+                                               graph=False, device="cpu")
+        q_proj = model.model.layers[0].self_attn.q_proj
+        q.put((rank, n_groups, bool(torch.equal(hist, ref_hist)), int((hist[:, 6:13] != 0).sum()),
+               isinstance(q_proj, RowShardedLinear4bit) and q_proj.gather))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tp_mode,batch", [("gather", 1), ("pair", 2)])
+def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch):
+    """bench.py --gpus 2 exactly as the driver runs it, on gloo world 2 with the
+    oracle as each shard's local product: the default strong-scaling layout
+    (one bs=1 stream, every Linear4bit row-split + all-gather) and the
+    weak-scaling extra (two streams, Megatron pairing).  The greedy tokens of 7
+    decode steps equal the unsharded model's on every rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
+        os.environ.get("PYTHONPATH", "")
+    procs = [ctx.Process(target=_bench_layout_worker, args=(r, world, port, q, tp_mode, batch))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, n_groups, same, n_tok, gathers in res:
+        assert n_groups == 4, (rank, n_groups)
+        assert same, f"rank {rank}: sharded greedy tokens differ from the unsharded model"
+        assert n_tok > 0
+        assert gathers == (tp_mode == "gather")
+
+
+def _gemv_hook(x, mod):
+    """Test hook: a shard's local GEMV with the reference's fp32 weight products
+    (kernels.cu:1169: code[nibble] * absmax in fp32), output in x's dtype."""
+    from quantizations_amd.parallel import consumer_absmax
+
+    st = mod.state
+    M, K = int(st.shape[0]), int(st.shape[1])
+    b = mod.packed.reshape(-1).numpy()
+    nib = np.stack([b >> 4, b & 15], axis=1).reshape(-1)
+    am = consumer_absmax(st).numpy()[mod.block_base:mod.block_base + M * K // st.blocksize]
+    W = (st.code.numpy()[nib] * np.repeat(am, st.blocksize)).astype(np.float32).reshape(M, K)
+    y = torch.from_numpy(x.reshape(-1, K).double().numpy() @ W.T.astype(np.float64))
+    if mod.bias is not None:
+        y = y + mod.bias.double()
+    return y.reshape(*x.shape[:-1], M).to(x.dtype)
+
+
+def _rowpar_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from quantizations_amd.parallel import RowParallelLinear4bit
+
+        M, K = 256, 1024
+        full, st, b = _full_module(M, K, "nf4", seed=31, bias=True)
+        layer = RowParallelLinear4bit(full, local_matmul=_gemv_hook)
+        Kp = K // world
+        g = torch.Generator().manual_seed(4)
+        x = (torch.randn(1, 1, K, generator=g) * 4).to(torch.float16)
+        Kp = K // world
+        y = layer(x[..., rank * Kp:(rank + 1) * Kp])
+        # emulation: each rank's partial rounded to fp16 once, summed in fp32, rounded once
+        from quantizations_amd.parallel import consumer_absmax
+        qs = full.weight.quant_state
+        pk = full.weight.data.reshape(-1).numpy()
+        nib = np.stack([pk >> 4, pk & 15], axis=1).reshape(-1)
+        W = (qs.code.numpy()[nib] * np.repeat(consumer_absmax(qs).numpy(), 64)).astype(np.float32).reshape(M, K)
+        xd = x.reshape(-1).double().numpy()
+        parts = [(xd[r * Kp:(r + 1) * Kp] @ W[:, r * Kp:(r + 1) * Kp].T.astype(np.float64)
+                  + (b.double().numpy() if r == 0 else 0.0)).astype(np.float16) for r in range(world)]
+        emu = np.sum(np.stack(parts).astype(np.float32), axis=0, dtype=np.float32).astype(np.float16)
+        q.put((rank, y.dtype == torch.float16, bool(np.array_equal(y.reshape(-1).numpy(), emu))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_parallel_fp32_allreduce_within_fp16_rounding():
+    """Row-parallel o/down layer at world 2 with fp16 activations: each rank's
+    fp16 partial is summed in fp32 and rounded to fp16 ONCE (an fp16 all-reduce
+    would add one more rounding per rank beyond two).  Bit-exact against that
+    emulation."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
+        os.environ.get("PYTHONPATH", "")
+    procs = [ctx.Process(target=_rowpar_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, is_half, same in res:
+        assert is_half
+        assert same, f"rank {rank}: row-parallel output is not the fp32 sum of the fp16 partials"

@@ -122,3 +122,44 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     assert not rms_norm_supported(x, torch.ones(64))  # CPU tensors never reach the kernel
     q = torch.randn(1, 4, 3, 16)
     assert not rope_supported(q, q, torch.randn(1, 3, 16), torch.randn(1, 3, 16))
+
+
+def test_fuse_layer_ops_leaves_other_rotary_forms_alone():
+    """The rotary patch is limited to Llama/Mistral/Qwen2 attention modules whose
+    modeling module has the half-split rotate_half.  An attention class outside
+    the allow-list (here: a Cohere-style module with the interleaved
+    rotate_half) keeps its own apply_rotary_pos_emb, and so does an allow-listed
+    name whose module rotates interleaved."""
+    import sys
+    import types
+
+    from quantizations_amd.integration import _half_split_rotate, fuse_layer_ops, unfuse_layer_ops
+
+    def interleaved(x):  # modeling_cohere.py's rotate_half
+        x1, x2 = x[..., ::2], x[..., 1::2]
+        return torch.stack([-x2, x1], dim=-1).flatten(-2)
+
+    def apply_rotary_pos_emb(q, k, cos, sin, unsqueeze_dim=1):
+        return q, k
+
+    created = []
+    for modname, clsname in (("qz_fake_cohere", "CohereAttention"), ("qz_fake_llama_like", "LlamaAttention")):
+        mod = types.ModuleType(modname)
+        mod.rotate_half = interleaved
+        mod.apply_rotary_pos_emb = apply_rotary_pos_emb
+        cls = type(clsname, (torch.nn.Module,), {"__module__": modname})
+        mod.__dict__[clsname] = cls
+        sys.modules[modname] = mod
+        created.append((modname, cls))
+    try:
+        assert not _half_split_rotate(sys.modules["qz_fake_cohere"])
+        import transformers.models.llama.modeling_llama as ml
+        assert _half_split_rotate(ml)
+        model = torch.nn.Sequential(*[cls() for _, cls in created])
+        assert fuse_layer_ops(model, norm=False, mlp=False) == 0
+        for modname, _ in created:
+            assert sys.modules[modname].apply_rotary_pos_emb is apply_rotary_pos_emb
+        unfuse_layer_ops(model)
+    finally:
+        for modname, _ in created:
+            sys.modules.pop(modname, None)

@@ -224,10 +224,12 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
     stream = torch.cuda.current_stream().cuda_stream
     fn = _lib.lib.qz_gemv_4bit
 
+    qt_flags = [_lib.NF4]
+
     def launch(i):
         p, qa, a2 = sets[i % copies]
-        rc = fn(4096, 4096, x.data_ptr(), _lib.DT_F16, p.data_ptr(), _lib.NF4, 64, 0, qa.data_ptr(), a2.data_ptr(),
-                code2.data_ptr(), off.data_ptr(), 256, 0, 0, 0, y.data_ptr(), stream)
+        rc = fn(4096, 4096, x.data_ptr(), _lib.DT_F16, p.data_ptr(), qt_flags[0], 64, 0, qa.data_ptr(),
+                a2.data_ptr(), code2.data_ptr(), off.data_ptr(), 256, 0, 0, 0, y.data_ptr(), stream)
         if rc:
             raise RuntimeError(f"qz_gemv_4bit rc={rc}")
 
@@ -264,6 +266,13 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(b2b)
     b2b_us = e0.elapsed_time(e1) * 1e3 / iters
+    # the same launches with exact (fp32) NF4 codes (QZ_EXACT_CODES: hi + lo fp16 code split)
+    qt_flags[0] = _lib.NF4 | _lib.EXACT_CODES
+    for i in range(copies):
+        launch(i)
+    blocked(b2b)
+    exact_us = e0.elapsed_time(e1) * 1e3 / iters
+    qt_flags[0] = _lib.NF4
     # one-shot read floor of the same 8.39 MB packed weight (same rotation, same timing method)
     sink = torch.zeros(1, dtype=torch.int32, device=dev)
     floor_fn = _lib.lib.qz_bench_read_floor
@@ -294,7 +303,49 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(empty)
     empty_us = e0.elapsed_time(e1) * 1e3 / iters
+    GEMV_EXTRA["exact_codes_launch_us"] = round(exact_us, 3)
     return statistics.mean(us), statistics.median(us), b2b_us, floor_us, empty_us
+
+
+GEMV_EXTRA = {}
+
+
+@torch.inference_mode()
+def gemv_parity():
+    """Decode-GEMV accuracy at the Llama-3-8B shapes (NF4 + double quant, fp16 x):
+    rel err ||y - y_ref|| / ||y_ref|| with y_ref the fp64 product of the fp32
+    dequantised weight (= the reference's fp32 weight products kernels.cu:1169;
+    dequantize_4bit(fp32) is pinned bit-exact to the oracle in tests/), for the
+    default fp16-code table and the exact-code variant; fp16 output (the bench
+    config) and fp32 output (x in fp32: the code error is not hidden by the
+    output rounding)."""
+    from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
+
+    dev = torch.device("cuda")
+    res = {}
+    for (M, K) in [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)]:
+        torch.manual_seed(M + K)
+        W = (torch.randn(M, K, device=dev) * 0.02).half()
+        packed, st = quantize_4bit(W, quant_type="nf4")
+        del W
+        wd = dequantize_4bit(packed, st, out_dtype=torch.float32).t().double()   # [M, K]
+        x = torch.randn(K, device=dev).half()
+        ref = wd @ x.double()
+        row = {}
+        for name, ex in (("fp16_codes", False), ("exact_codes", True)):
+            for xdt in (torch.float16, torch.float32):
+                y = gemv_4bit(x.to(xdt).reshape(1, K), packed, state=st, exact_codes=ex).reshape(-1).double()
+                row[f"{name}_{'f16' if xdt == torch.float16 else 'f32'}_out"] = \
+                    float(f"{((y - ref).norm() / ref.norm()).item():.3e}")
+        res[f"{M}x{K}"] = row
+        del wd, packed, st
+    return {"rel_err_vs_fp32_weight_products": res, "tolerance": 1e-3,
+            "default": "exact_codes" if _exact_default() else "fp16_codes"}
+
+
+def _exact_default() -> bool:
+    from quantizations_amd import core
+    return core.GEMV_EXACT_CODES
 
 
 def gemv_alg_bytes(shapes, dq: bool = True, x_bytes: int = 2, y_bytes: int = 2) -> int:
@@ -432,33 +483,70 @@ def prefill_sweep(Ts=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 1
     return {"shape": "4096x4096 nf4 dq", "us": res}
 
 
-def cpu_baseline(target_s: float = 12.0):
+def _cpu_model() -> str:
+    """`lscpu` model name of the host (falls back to /proc/cpuinfo)."""
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(runs: int = 20, warmups: int = 3):
+    """config #1 on the host cores -- Linear4bit(4096,4096)
+    NF4 + double quant, W ~ N(0, 0.02^2) fp16 (seed 0), x ~ N(0,1) fp16 (seed 1);
+    the oracle's CPU restatement (absmax double-dequant + LUT dequant to fp32,
+    then torch.matmul in fp32; the reference has no CPU path).  Median of
+    `runs` after `warmups`, for dequant+matmul and for the matmul alone."""
     import numpy as np
 
     import oracle
 
     # the GPU box exposes the whole machine's CPUs; its share is OMP_NUM_THREADS (16)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     torch.set_num_threads(cores)
-    g = torch.Generator().manual_seed(0)
-    W = (torch.randn(4096, 4096, generator=g) * 0.02).to(torch.float16)
-    x = torch.randn(4096, generator=g).to(torch.float16).float().numpy()
+    W = (torch.randn(4096, 4096, generator=torch.Generator().manual_seed(0)) * 0.02).to(torch.float16)
+    x16 = torch.randn(1, 1, 4096, generator=torch.Generator().manual_seed(1)).to(torch.float16)
+    x = x16.float().numpy().reshape(-1)
     st = oracle.quantize_4bit(W.float().numpy(), 64, "nf4", double_quant=True)
-    oracle.cpu_dequant_matmul(x, st)  # warm-up
-    ts = []
-    t_start = time.perf_counter()
-    while time.perf_counter() - t_start < target_s or len(ts) < 3:
-        t0 = time.perf_counter()
-        oracle.cpu_dequant_matmul(x, st)
-        ts.append(time.perf_counter() - t0)
-    layer_s = statistics.median(ts)
+
+    def timed(fn):
+        for _ in range(warmups):
+            fn()
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    full_s = timed(lambda: oracle.cpu_dequant_matmul(x, st))
+    Wf = oracle.cpu_dequant(st)
+    xt = torch.from_numpy(x).reshape(1, 4096)
+    mm_s = timed(lambda: xt @ Wf.t())
     elems_per_token = LLAMA3_8B["num_hidden_layers"] * sum(m * k for m, k in LAYER_SHAPES)
-    tok_s = 1.0 / (layer_s * elems_per_token / (4096 * 4096))
+    tok_s = 1.0 / (full_s * elems_per_token / (4096 * 4096))
     del np
     return {"value": round(tok_s, 5), "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"config #1: Linear4bit(4096,4096) NF4+DQ CPU dequant + torch.matmul fp32 "
-                      f"(oracle restatement), median of {len(ts)} runs = {layer_s * 1e3:.1f} ms/layer, "
-                      f"scaled by elements to the 224 Linear4bit layers of one Llama-3-8B token"}
+            "cpu_model": _cpu_model(),
+            "dequant_matmul_ms": round(full_s * 1e3, 3), "matmul_alone_ms": round(mm_s * 1e3, 3),
+            "runs": runs, "warmups": warmups,
+            "sample": f"config #1: Linear4bit(4096,4096) NF4+DQ, CPU dequant + torch.matmul fp32 (oracle "
+                      f"restatement of kernels.cu/core.py), median of {runs} runs after {warmups} warm-ups = "
+                      f"{full_s * 1e3:.1f} ms per layer ({mm_s * 1e3:.2f} ms of it the matmul alone); value = "
+                      f"that layer time scaled by weight count to the 224 Linear4bit layers of one Llama-3-8B "
+                      f"token (extrapolated, not a decode run)"}
 
 
 def main():
@@ -519,7 +607,7 @@ def main():
     if args.gemv_only:
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         print(json.dumps({"gemv_4096_us_mean": mean_us, "gemv_4096_us_median": med_us, "back_to_back_us": b2b_us,
-                          "read_floor_us": floor_us, "empty_launch_us": empty_us,
+                          "read_floor_us": floor_us, "empty_launch_us": empty_us, **GEMV_EXTRA,
                           "achieved_GBs": GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9}), flush=True)
         return
 
@@ -583,6 +671,7 @@ def main():
                       "global_batch": args.batch * world, "decode": wmode, "parallelism": parallelism("pair")}
 
     roof = None
+    parity = None
     if rank == 0 and not args.no_roofline:
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         # average launch duration = HIP events around `iters` back-to-back launches on
@@ -606,7 +695,9 @@ def main():
                 "empty_launch_us": round(empty_us, 3),
                 "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
                                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "exact_codes_launch_us": GEMV_EXTRA.get("exact_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline()}
+        parity = gemv_parity()
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:
@@ -629,7 +720,7 @@ def main():
                        "stream_batch": 1, "decode": mode,
                        "parallelism": parallelism(tp_mode),
                        "projection_groups": n_groups, "layer_ops": n_layer_ops},
-            "roofline": roof, "cpu_baseline": cpu, "prefill_config4": prefill,
+            "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         if extra_weak is not None:
             line["weak_scaling_extra"] = extra_weak

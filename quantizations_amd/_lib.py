@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("QZ_LIB_PATH", os.path.join(HERE, "libquantizations.so
 DT_F16, DT_BF16, DT_F32 = 0, 1, 2
 FP4, NF4 = 0, 1
 QUANT_TYPES = {"fp4": FP4, "nf4": NF4}
+EXACT_CODES = 0x100  # QZ_EXACT_CODES: GEMV quant_type flag, decode with the fp32 codes
 
 _STATUS = {
     -1: "invalid argument (null pointer or negative size)",

@@ -362,10 +362,25 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, blocksi
     return out.t()
 
 
+# Decode GEMV codebook precision.  The reference GEMV multiplies by its fp32
+# quant_map (kernels.cu:1115-1120).  The default byte-table decode holds the
+# NF4 codes as fp16 (<= 2.4e-4 relative per code); exact codes
+# split each fp32 code into two fp16 parts (~2^-23 relative: fp32-class) at the
+# cost of one more dot product per weight pair.  FP4 is exact either way.
+GEMV_EXACT_CODES = os.environ.get("QZ_GEMV_EXACT_CODES", "1") == "1"
+
+
+def _gemv_quant_type(quant_type: str, exact_codes: Optional[bool]) -> int:
+    exact = GEMV_EXACT_CODES if exact_codes is None else exact_codes
+    return _lib.QUANT_TYPES[quant_type] | (_lib.EXACT_CODES if exact else 0)
+
+
 def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
-              state=None, bias: Optional[Tensor] = None, block_base: int = 0) -> Tensor:
+              state=None, bias: Optional[Tensor] = None, block_base: int = 0,
+              exact_codes: Optional[bool] = None) -> Tensor:
     """Batch-1 4-bit GEMV (reference core.py:426-504) as ONE fused kernel:
-    y = x . W^T (+ bias), W from `state`; out dtype = A.dtype."""
+    y = x . W^T (+ bias), W from `state`; out dtype = A.dtype.  `exact_codes`
+    (default GEMV_EXACT_CODES) decodes with the fp32 codebook values."""
     if state is None:
         raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
     if A.numel() != A.shape[-1]:
@@ -380,13 +395,13 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     A = A.contiguous()
     if bias is not None and bias.dtype != A.dtype:
         bias = bias.to(A.dtype)
-    check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _lib.QUANT_TYPES[state.quant_type],
+    check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _gemv_quant_type(state.quant_type, exact_codes),
                            state.blocksize, *state.scale_args(), block_base, 0, ptr(bias), ptr(out),
                            _lib.stream_of(A)), "gemv_4bit")
     return out
 
 
-def gemv_4bit_grouped(A: Tensor, items) -> list:
+def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> list:
     """Several batch-1 4-bit GEMVs that share the input vector A, in ONE launch
     (qz_gemv_4bit_grouped).  items: sequence of
     (B, state, bias[, block_base[, out]]) with equal K, quant_type, blocksize
@@ -425,7 +440,8 @@ def gemv_4bit_grouped(A: Tensor, items) -> list:
         outs.append(y)
     bs2 = int(s0.state2.blocksize) if s0.nested else 0
     check(lib.qz_gemv_4bit_grouped(len(items), ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
-                                   _lib.QUANT_TYPES[s0.quant_type], s0.blocksize, bs2, 0, _lib.stream_of(A)),
+                                   _gemv_quant_type(s0.quant_type, exact_codes), s0.blocksize, bs2, 0,
+                                   _lib.stream_of(A)),
           "gemv_4bit_grouped")
     return outs
 

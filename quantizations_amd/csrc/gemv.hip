@@ -34,8 +34,16 @@
 //    weight, half of them half-rate v_perm: VALU-issue-bound on gfx950.
 // Products: v_dot2_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
 // per 32-element chunk the fp32 dot is scaled by the block absmax with one
-// FMA.  fp32/bf16 activations are split into hi+lo fp16 halves (x = xh + xl,
-// 2^-22 relative) so they keep fp32-class accuracy.
+// FMA.  fp32/bf16 activations are split into hi+lo fp16 halves (x = xh + xl)
+// after a per-lane power-of-two pre-scale that puts the chunk's largest |x| in
+// [2^14, 2^15): no saturation above 65504, no flush below 2^-24, ~2^-21 of
+// the chunk maximum (undone exactly on the fp32 dot).
+// Exact codes (CL): a runtime codebook (`lut`, the reference ABI's fp32
+// quant_map, kernels.cu:1115-1120) is NOT rounded to fp16: each code c is
+// stored as c * 2^S = ch + cl, two fp16 values (~2^-23 relative: fp32-class),
+// in a 64-bit table entry (hi pair, lo pair) read with one ds_read_b64, and
+// the dot takes ch*x + cl*x.  S (power of two, from max|code|) is undone on
+// the output.
 #include "common.h"
 
 namespace qz {
@@ -57,6 +65,13 @@ enum {
 // (dword e*32 + j), and lane l reads copy l % 32: never a bank conflict.
 constexpr int kTabCopies = 32;
 constexpr int kTabDwords = 256 * kTabCopies;  // 32 KiB
+// CL (exact codes): 64-bit entries (hi pair, lo pair), 16 copies -> the same
+// 128 B per byte value and 32 KiB, so the byte -> address computation and the
+// occupancy are unchanged.  Lane l reads copy l % 16: a ds_read_b64 lane group
+// (32 lanes, bank = dword mod 64) then holds two lanes per copy, which collide
+// only when their byte values have the same parity (entry stride 32 dwords):
+// 1.5-way on average.
+constexpr int kTabCopiesCL = 16;
 
 // The byte tables of the two built-in codebooks, computed at compile time and
 // stored once in device memory with each entry repeated 4 times (one 16-B
@@ -94,11 +109,39 @@ constexpr ByteTable make_nf4_table() {
 // FP4 x12: magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3} (exact fp16), sign in code bit 3 (code 8 = -0.0)
 constexpr uint16_t kFP4x12Bits[16] = {0x0000, 0x2C00, 0x4800, 0x4A00, 0x4400, 0x4600, 0x4000, 0x4200,
                                       0x8000, 0xAC00, 0xC800, 0xCA00, 0xC400, 0xC600, 0xC000, 0xC200};
+// exact NF4 codes (CL): c * 2^14 = hi + lo (fp16 each), entries {hi pair, lo pair} x 2
+constexpr int kNF4ExactShift = 14;
+constexpr float f16_value_c(uint16_t h) {  // normal-range values and +-0 only
+  const float sgn = (h & 0x8000u) ? -1.0f : 1.0f;
+  const int e = (h >> 10) & 31;
+  if (e == 0) return sgn * 0.0f;
+  float v = 1.0f + (float)(h & 0x3FFu) / 1024.0f;
+  for (int i = 15; i < e; ++i) v *= 2.0f;
+  for (int i = e; i < 15; ++i) v *= 0.5f;
+  return sgn * v;
+}
+constexpr ByteTable make_nf4_exact_table() {
+  uint16_t hi[16] = {}, lo[16] = {};
+  for (int i = 0; i < 16; ++i) {
+    const float c = kNF4Host[i] * (float)(1 << kNF4ExactShift);  // exact (power of two)
+    hi[i] = f16_bits_rne_c(c);
+    lo[i] = f16_bits_rne_c(c - f16_value_c(hi[i]));               // the residual is exact in fp32
+  }
+  ByteTable t{};
+  for (int e = 0; e < 256; ++e) {
+    const uint32_t h = (uint32_t)hi[e >> 4] | ((uint32_t)hi[e & 15] << 16);
+    const uint32_t l = (uint32_t)lo[e >> 4] | ((uint32_t)lo[e & 15] << 16);
+    t.v[4 * e + 0] = h; t.v[4 * e + 1] = l; t.v[4 * e + 2] = h; t.v[4 * e + 3] = l;
+  }
+  return t;
+}
 __device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
+__device__ const ByteTable g_byte_tab_nf4x = make_nf4_exact_table();
 __device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
 static_assert(f16_bits_rne_c(0.07958029955625534f) == 0x2D18, "fp16 RNE of an NF4 code");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 struct GemvParams {
   const unsigned char *B;
@@ -111,7 +154,8 @@ struct GemvParams {
   int M, K;
   int bs_log2, bs2_log2;
   float out_scale;
-  int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12) precomputed byte table; lut != nullptr builds in kernel
+  int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12), 2 = exact NF4 (CL) precomputed byte table;
+                     // lut != nullptr builds an exact (CL) table in kernel
   uint32_t tab[8];
 };
 
@@ -261,8 +305,11 @@ template <int MODE, int DT> struct XSlice {
     }
   }
 
-  // hi/lo half2 operands, pair order of MODE
-  __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1]) const {
+  // hi/lo half2 operands, pair order of MODE.  fp32/bf16: the chunk is first
+  // scaled by 2^se so that its largest |x| lies in [2^14, 2^15) (hi = rtz
+  // never saturates, lo never flushes); usc = 2^-se undoes it on the dot.
+  __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1], float &usc) const {
+    usc = 1.0f;
     if constexpr (DT == QZ_DT_F16) {
       if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
 #pragma unroll
@@ -288,6 +335,15 @@ template <int MODE, int DT> struct XSlice {
           f[2 * i + 1] = __uint_as_float(raw[i] & 0xFFFF0000u);
         }
       }
+      // chunk max |x| (v_max3_f32 with abs modifiers; NaN is ignored here and
+      // still propagates through the dot), its biased exponent E, se = 141 - E
+      float mx = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 32; i += 2) mx = fmaxf(mx, fmaxf(fabsf(f[i]), fabsf(f[i + 1])));
+      const int E = (int)(__float_as_uint(mx) >> 23);
+      const int se = min(141 - E, 100);                    // in [-114, 100]: both scales are normal
+      const float sc = __uint_as_float((uint32_t)(127 + se) << 23);
+      usc = __uint_as_float((uint32_t)(127 - se) << 23);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         int a[4], b[4];
@@ -298,8 +354,8 @@ template <int MODE, int DT> struct XSlice {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          // hi = rtz(f) (never overflows to inf below 65536), lo = rtz(f - hi); f - hi is exact
-          const float fa = f[8 * d + a[j]], fb = f[8 * d + b[j]];
+          // hi = rtz(f s) (|f s| < 2^15), lo = rtz(f s - hi); f s - hi is exact
+          const float fa = f[8 * d + a[j]] * sc, fb = f[8 * d + b[j]] * sc;
           const auto h = __builtin_amdgcn_cvt_pkrtz(fa, fb);
           const float ra = fa - (float)h.x, rb = fb - (float)h.y;
           hi[4 * d + j] = __builtin_bit_cast(uint32_t, h);
@@ -340,30 +396,35 @@ __device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)
 }
 
 // kModeTab: dot of one lane's 16-byte chunk through the LDS byte table.
-// `jb` = 4 * (lane % 32) selects the lane's bank-private copy.
+// `jb` selects the lane's bank-private copy: 4 * (lane % 32), or for CL
+// (64-bit exact-code entries) 8 * (lane % 16).  Both tables use 128 B per
+// byte value, so the address of byte m is (byte << 7) | jb either way.
 // (ABL: benchmark-only ablations -- 16 replaces the dot products by integer
 // adds, 32 replaces the table reads by the addresses themselves.)
-template <bool SPLIT, int ABL = 0>
+template <bool SPLIT, int ABL = 0, bool CL = false>
 __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&hi)[16],
                                                const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t *s_tab,
                                                uint32_t jb) {
   const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
   const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  uint32_t v[16];
+  uint32_t v[16], vl[CL ? 16 : 1];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    // byte m of w, times 128 (the 32-dword stride of one entry), plus the copy
-    const uint32_t a0 = ((w[d] << 7) & 0x7F80u) | jb;
-    const uint32_t a1 = ((w[d] >> 1) & 0x7F80u) | jb;
-    const uint32_t a2 = ((w[d] >> 9) & 0x7F80u) | jb;
-    const uint32_t a3 = ((w[d] >> 17) & 0x7F80u) | jb;
-    if constexpr ((ABL & 32) != 0) {
-      v[4 * d + 0] = a0; v[4 * d + 1] = a1; v[4 * d + 2] = a2; v[4 * d + 3] = a3;
-    } else {
-      v[4 * d + 0] = *reinterpret_cast<const uint32_t *>(tb + a0);
-      v[4 * d + 1] = *reinterpret_cast<const uint32_t *>(tb + a1);
-      v[4 * d + 2] = *reinterpret_cast<const uint32_t *>(tb + a2);
-      v[4 * d + 3] = *reinterpret_cast<const uint32_t *>(tb + a3);
+    // byte m of w, times 128 (the stride of one entry), plus the copy
+    const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
+                           ((w[d] >> 9) & 0x7F80u) | jb, ((w[d] >> 17) & 0x7F80u) | jb};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      if constexpr ((ABL & 32) != 0) {
+        v[4 * d + m] = a[m];
+        if constexpr (CL) vl[4 * d + m] = a[m] ^ 1u;
+      } else if constexpr (CL) {
+        const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a[m]);
+        v[4 * d + m] = e.x;
+        vl[4 * d + m] = e.y;
+      } else {
+        v[4 * d + m] = *reinterpret_cast<const uint32_t *>(tb + a[m]);
+      }
     }
   }
   if constexpr ((ABL & 16) != 0) {
@@ -378,12 +439,10 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
   float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    if (i & 1) s1 = dot2(v[i], hi[i], s1);
-    else s0 = dot2(v[i], hi[i], s0);
-    if constexpr (SPLIT) {
-      if (i & 1) s1 = dot2(v[i], lo[i], s1);
-      else s0 = dot2(v[i], lo[i], s0);
-    }
+    float &acc = (i & 1) ? s1 : s0;
+    acc = dot2(v[i], hi[i], acc);
+    if constexpr (CL) acc = dot2(vl[i], hi[i], acc);   // code residual x x_hi
+    if constexpr (SPLIT) acc = dot2(v[i], lo[i], acc);  // code_hi x x residual
   }
   return s0 + s1;
 }
@@ -429,12 +488,38 @@ __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t
 // 8-lane store group covers all 32 banks.  (Loading 8 pieces per thread to
 // make every store address an immediate offset was measured slower: the
 // extra loads delay the first weight loads.)
-__device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u32x4 &v) {
-  const uint32_t e = threadIdx.x;
+__device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u32x4 &v,
+                                                       const uint32_t e = threadIdx.x) {
 #pragma unroll
   for (int i = 0; i < kTabCopies / 4; ++i) {
     const uint32_t piece = (e + (uint32_t)i) & (kTabCopies / 4 - 1);
     reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = v;
+  }
+}
+
+// Exponent S (power of two) for a runtime codebook: max|code| * 2^S lies in
+// [2^14, 2^15), so every code c * 2^S splits into two normal fp16 values
+// ch + cl with ~2^-23 relative error (an all-zero or non-finite book: S = 0).
+__device__ __forceinline__ int lut_shift(const float *lut) {
+  float mx = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(lut[i]));
+  const int E = (int)(__float_as_uint(mx) >> 23);
+  if (mx == 0.0f || E == 255) return 0;
+  return max(-100, min(141 - E, 100));
+}
+
+// Builds the CL (exact-code) byte table from a runtime fp32 codebook: entry
+// e = {hi pair, lo pair} of (code[e >> 4], code[e & 15]) * 2^S, 16 copies.
+template <int NT>
+__device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const float *lut, int S) {
+  for (int e = threadIdx.x; e < 256; e += NT) {
+    const float ca = ldexpf(lut[e >> 4], S), cb = ldexpf(lut[e & 15], S);
+    const uint32_t h = cvt_pk_f16_rne(ca, cb);
+    const float ra = ca - (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu));
+    const float rb = cb - (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
+    const uint32_t l = cvt_pk_f16_rne(ra, rb);
+    store_byte_table_entry(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
   }
 }
 
@@ -520,8 +605,10 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
   }
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false>
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
+          bool CL = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
+  static_assert(!CL || MODE == kModeTab, "exact codes need the byte-table decode");
   QZ_STAMP_DECL;
   QZ_STAMP(0);
   const GemvParams p = load_params(p_in);
@@ -556,8 +643,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   u32x4 tab_entry = {0u, 0u, 0u, 0u};
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
-    if (!p.lut && threadIdx.x < 256)
-      tab_entry = reinterpret_cast<const u32x4 *>((p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4)->v)[threadIdx.x];
+    if (!p.lut && threadIdx.x < 256) {
+      const ByteTable *bt = CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4);
+      tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
+    }
   }
   // 1c. XL: this thread's share of x (<= kXLChunks 16-B chunks), also ahead of the weights
   constexpr int kXLChunks = XL ? 8 : 1;
@@ -588,7 +677,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
   }
   uint32_t t[8];
-  if (p.lut) {  // runtime codebook -> fp16 byte tables (wave-uniform, once)
+  if (MODE != kModeTab && p.lut) {  // register decodes (microbenchmarks): runtime codebook -> fp16 byte planes
 #pragma unroll
     for (int i = 0; i < 8; ++i) t[i] = 0;
 #pragma unroll
@@ -601,13 +690,26 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 #pragma unroll
     for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
   }
+  // output scale: the codebook's (FP4 x12: 1/12; exact NF4: 2^-14), or for a
+  // runtime codebook (always exact codes) 2^-S of its in-kernel split
+  float out_scale = p.out_scale;
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if (p.lut) build_byte_table<NW * 64>(s_tab, t);
-    else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
+    if constexpr (CL) {
+      if (p.lut) {
+        const int S = lut_shift(p.lut);
+        out_scale = ldexpf(1.0f, -S);
+        build_byte_table_exact<NW * 64>(s_tab, p.lut, S);
+      } else if (threadIdx.x < 256) {
+        store_byte_table_entry(s_tab, tab_entry);
+      }
+    } else {
+      if (p.lut) build_byte_table<NW * 64>(s_tab, t);
+      else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
+    }
   }
   if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
   QZ_STAMP(1);
-  const uint32_t jb = (uint32_t)(lane & 31) << 2;
+  const uint32_t jb = CL ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2;
 
   float acc[R];
 #pragma unroll
@@ -621,15 +723,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   auto consume = [&](const StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &c) {
     if constexpr (XL) const_cast<StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &>(c).xs.load_lds(s_x, c.xb);
     uint32_t hi[16], lo[kSplit ? 16 : 1];
-    c.xs.prepare(hi, lo);
+    float usc;
+    c.xs.prepare(hi, lo, usc);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float am;
       if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
       else am = c.a[r];
       am = c.on ? am : 0.0f;
+      if constexpr (kSplit) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
-      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL>(c.wv[r], hi, lo, s_tab, jb);
+      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, CL>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
     }
@@ -679,7 +783,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       for (int r = 0; r < R; ++r) {
         const int row = row0 + r;
         if (row < p.M) {
-          float o = v[r] * p.out_scale;
+          float o = v[r] * out_scale;
           if (p.bias) o += load_f32<DT>(p.bias, row);
           store_f32<DT>(p.y, row, o);
         }
@@ -702,16 +806,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       float v = 0.0f;
 #pragma unroll
       for (int k = 0; k < WK; ++k) v += s_part[g * WK + k][r];
-      v *= p.out_scale;
+      v *= out_scale;
       if (p.bias) v += load_f32<DT>(p.bias, row);
       store_f32<DT>(p.y, row, v);
     }
   }
 }
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false>
+template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
+          bool CL = false>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL>(p, blockIdx.x);
 }
 
 // Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
@@ -726,7 +831,7 @@ struct GemvGroup {
   int nseg;
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, bool FS>
+template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -739,7 +844,7 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS>(seg, b - start);
+  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL>(seg, b - start);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -824,12 +929,12 @@ static int ilog2(long long v) {
 }
 
 // Geometries choose_geometry can return: (R, WK) in {(4,1), (2,1), (1,1), (1,2), (1,4)}.
-template <int MODE, bool DQ, int DT, bool FS>
+template <int MODE, bool DQ, int DT, bool FS, bool CL>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
 #define QZ_GV(RR, WW) \
-  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS>), dim3(grid), dim3(256), 0, s, p)
+  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL>), dim3(grid), dim3(256), 0, s, p)
   if (R == 4) QZ_GV(4, 1);
   else if (R == 2) QZ_GV(2, 1);
   else if (WK == 1) QZ_GV(1, 1);
@@ -838,14 +943,22 @@ static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
 #undef QZ_GV
 }
 
-template <int MODE, bool DQ, bool FS>
+template <int MODE, bool DQ, bool FS, bool CL>
 static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_t s) {
   switch (dtype) {
-    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16, FS>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16, FS>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32, FS>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16, FS, CL>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16, FS, CL>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32, FS, CL>(p, R, WK, s); return QZ_OK;
   }
   return QZ_ERR_DTYPE;
+}
+
+template <bool CL>
+static int dispatch_tab(const GemvParams &p, int dtype, bool dq, bool fs, int R, int WK, hipStream_t s) {
+  if (fs) return dq ? dispatch_dt<kModeTab, true, true, CL>(p, dtype, R, WK, s)
+                    : dispatch_dt<kModeTab, false, true, CL>(p, dtype, R, WK, s);
+  return dq ? dispatch_dt<kModeTab, true, false, CL>(p, dtype, R, WK, s)
+            : dispatch_dt<kModeTab, false, false, CL>(p, dtype, R, WK, s);
 }
 
 }  // namespace qz
@@ -883,10 +996,20 @@ static bool full_steps(int K, int blocksize, int blocksize2, bool dq, long long 
 
 // Decode tables for the byte-table kernel: the 16-entry codebook as fp16 byte
 // planes (a runtime `lut` is converted in kernel, so its planes stay zero).
-static void set_tables(int quant_type, const float *lut, GemvParams *p) {
+// Exact codes (CL): the built-in NF4 table holds code * 2^14 as hi + lo.
+static void set_tables(int quant_type, const float *lut, bool cl, GemvParams *p) {
   build_tables(kModeTab, lut ? QZ_NF4 : quant_type, p->tab, &p->out_scale);
-  p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : 0;
+  p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : (cl ? 2 : 0);
   if (lut) p->out_scale = 1.0f;
+  else if (cl) p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
+}
+
+// Exact codes: a runtime codebook is always decoded exactly (the reference
+// ABI's fp32 quant_map); QZ_EXACT_CODES asks for it with the built-in NF4 book.
+// The built-in FP4 book x12 is exact in fp16 already.
+static bool exact_codes(int quant_type_flags, const float *lut) {
+  if (lut) return true;
+  return (quant_type_flags & QZ_EXACT_CODES) && (quant_type_flags & ~QZ_EXACT_CODES) == QZ_NF4;
 }
 
 // Validates one GEMV's arguments and fills its kernel parameters (everything
@@ -896,6 +1019,7 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
                        const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
                        void *y, GemvParams *p, bool *vec_ok) {
   if (!x || !B || !y || M < 0 || K < 0) return QZ_ERR_ARG;
+  quant_type &= ~QZ_EXACT_CODES;
   if ((absmax == nullptr) == (qabsmax == nullptr)) return QZ_ERR_ARG;
   const bool dq = qabsmax != nullptr;
   if (dq && (!absmax2 || !code2 || !offset)) return QZ_ERR_ARG;
@@ -934,6 +1058,8 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   if (M == 0) return QZ_OK;
   const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
+  const bool cl = exact_codes(quant_type, lut);
+  quant_type &= ~QZ_EXACT_CODES;
 
   if (!vec_ok) {
     const unsigned grid = (unsigned)((M + 3) / 4);
@@ -952,12 +1078,9 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
 
   int R, WK;
   choose_geometry(M, K, &R, &WK);
-  set_tables(quant_type, lut, &p);
-  int rc;
-  if (full_steps(K, blocksize, blocksize2, dq, block_base))
-    rc = dq ? dispatch_dt<kModeTab, true, true>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false, true>(p, dtype, R, WK, s);
-  else
-    rc = dq ? dispatch_dt<kModeTab, true, false>(p, dtype, R, WK, s) : dispatch_dt<kModeTab, false, false>(p, dtype, R, WK, s);
+  set_tables(quant_type, lut, cl, &p);
+  const bool fs = full_steps(K, blocksize, blocksize2, dq, block_base);
+  const int rc = cl ? dispatch_tab<true>(p, dtype, dq, fs, R, WK, s) : dispatch_tab<false>(p, dtype, dq, fs, R, WK, s);
   if (rc != QZ_OK) return rc;
   QZ_LAUNCH_CHECK();
   return QZ_OK;
@@ -968,6 +1091,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
   GemvGroup g;
   g.nseg = nseg;
+  const bool cl = exact_codes(quant_type, lut);
   bool all_vec = true;
   long long total_m = 0;
   const bool dq = segs[0].qabsmax != nullptr;
@@ -996,7 +1120,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
-    set_tables(quant_type, lut, &g.seg[i]);
+    set_tables(quant_type & ~QZ_EXACT_CODES, lut, cl, &g.seg[i]);
     g.start[i] = blocks;
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }
@@ -1004,8 +1128,13 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   bool all_fs = true;
   for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;
-#define QZ_GR(DQ_, DT_, RR, WW, FS_) \
-  hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_>), dim3(blocks), dim3(256), 0, s, g)
+#define QZ_GR(DQ_, DT_, RR, WW, FS_)                                                                          \
+  do {                                                                                                      \
+    if (cl) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, true>), dim3(blocks),  \
+                               dim3(256), 0, s, g);                                                         \
+    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, false>), dim3(blocks),    \
+                            dim3(256), 0, s, g);                                                            \
+  } while (0)
 #define QZ_GR_RW(DQ_, DT_, FS_)                                      \
   do {                                                               \
     if (R == 4) QZ_GR(DQ_, DT_, 4, 1, FS_);                          \

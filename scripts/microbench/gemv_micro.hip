@@ -49,7 +49,8 @@ __global__ __launch_bounds__(NW * 64) void k_gemv_4bit_sl(GemvParams p_in) {
   for (int i = 0; i < NSW; ++i) {
     StepLoads<MODE, DQ, DT, R, false, 0> &c = ld[i & 1];
     uint32_t hi[16], lo[kSplit ? 16 : 1];
-    c.xs.prepare(hi, lo);
+    float usc;
+    c.xs.prepare(hi, lo, usc);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float am;

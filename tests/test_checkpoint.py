@@ -152,3 +152,52 @@ def test_tiny_llama_checkpoint_round_trip_gpu(tmp_path):
     with torch.no_grad():
         out = other(input_ids=ids).logits
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+def test_oracle_built_checkpoint_loaded_on_gpu_matches_oracle(tmp_path, orc, qt):
+    """A safetensors file written from ORACLE-built quant states (packed bytes,
+    qabsmax, absmax2, offset under the core.py:29-42 keys) -- no GPU kernel
+    produced any of it -- loaded with load_quantized onto the GPU: Linear4bit
+    decode (the fused GEMV, exact codes and default table), prefill, and
+    gemv_4bit on the loaded state all match oracle.gemv of the same bytes."""
+    from safetensors.torch import save_file
+
+    from quantizations_amd.core import gemv_4bit
+    from quantizations_amd.integration import load_quantized
+    from quantizations_amd.modules import Linear4bit
+
+    shapes = {"up": (384, 1024), "down": (1024, 384 * 2)}
+    sd, states = {}, {}
+    for i, (name, (M, K)) in enumerate(shapes.items()):
+        packed, qs = _oracle_state(M, K, qt, True, seed=40 + i)
+        sd[f"{name}.weight"] = packed
+        for k, v in qs.as_dict(packed=True).items():
+            sd[f"{name}.weight.{k}"] = v
+        W = (torch.randn(M, K, generator=torch.Generator().manual_seed(40 + i)) * 0.02).half()
+        states[name] = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=True)
+        assert np.array_equal(packed.numpy().ravel(), states[name].packed)
+    path = str(tmp_path / "oracle.safetensors")
+    save_file(sd, path)
+
+    model = torch.nn.Sequential()
+    model.add_module("up", torch.nn.Linear(1024, 384, bias=False))
+    model.add_module("down", torch.nn.Linear(768, 1024, bias=False))
+    load_quantized(model, path, device="cuda")
+    for name, (M, K) in shapes.items():
+        lin = getattr(model, name)
+        assert isinstance(lin, Linear4bit) and lin.weight.is_cuda and lin.weight.quant_type == qt
+        o = states[name]
+        x = torch.randn(1, 1, K, generator=torch.Generator().manual_seed(M)).half()
+        yref = orc.gemv(x.float().numpy().ravel(), o)
+        y = lin(x.cuda()).float().cpu().numpy().ravel()
+        rel = np.linalg.norm(y - yref) / np.linalg.norm(yref)
+        assert rel <= 1e-3, (name, rel)
+        ye = gemv_4bit(x.float().cuda(), lin.weight, state=lin.weight.quant_state, exact_codes=True)
+        rel_e = np.linalg.norm(ye.cpu().numpy().ravel() - yref) / np.linalg.norm(yref)
+        assert rel_e <= 1e-5, (name, rel_e)
+        X = torch.randn(3, 7, K, generator=torch.Generator().manual_seed(K)).half()
+        Yref = X.reshape(-1, K).double().numpy() @ orc.dequantize(o).astype(np.float16).astype(np.float64).T
+        Y = lin(X.cuda()).double().cpu().numpy().reshape(-1, M)
+        assert np.linalg.norm(Y - Yref) / np.linalg.norm(Yref) <= 1e-3

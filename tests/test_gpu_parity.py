@@ -346,8 +346,9 @@ def test_gemv_llama70b_shapes_vs_fp64_of_dequant(M, K):
 def test_linear4bit_bf16_fp32_activations_and_compute_dtype(orc, act):
     """Linear4bit with bf16/fp32 inputs (compute_dtype follows the input, reference
     modules.py:112-122): decode and prefill outputs keep the input dtype.  Decode is
-    checked against the fp16 dequantised weight (the GEMV keeps fp16 codes x fp32
-    scales); prefill against the weight in the activation dtype that the kernels
+    checked against the reference's fp32 weight products (kernels.cu:1169: the fp32
+    dequantised weight, bit-exact to the oracle); prefill against the weight in the
+    activation dtype that the kernels
     multiply: dequantize_4bit(out_dtype=act), i.e. bf16(code*absmax) rounded once.
     (The reference's bf16 path multiplies W.to(bf16) of the fp16 dequant, modules.py:64,
     a double rounding that differs by one bf16 ulp on ~1/16 of the weights -- the
@@ -360,7 +361,7 @@ def test_linear4bit_bf16_fp32_activations_and_compute_dtype(orc, act):
     m.weight = qa.Params4bit(lin.weight.data.half(), requires_grad=False, quant_type="nf4", module=m)
     m.bias = torch.nn.Parameter(lin.bias.data.clone(), requires_grad=False)
     m = m.to(DEV)
-    Wd = m.dequantize().double()
+    Wd = qa.dequantize_4bit(m.weight, m.weight.quant_state, out_dtype=torch.float32).t().double()
     for shape in ((1, 1, 1024), (3, 5, 1024)):
         x = torch.randn(*shape, generator=torch.Generator().manual_seed(sum(shape))).to(act)
         y = m(x.to(DEV))

@@ -224,7 +224,10 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
     stream = torch.cuda.current_stream().cuda_stream
     fn = _lib.lib.qz_gemv_4bit
 
-    qt_flags = [_lib.NF4]
+    from quantizations_amd import core
+    prod_qt = _lib.NF4 | (_lib.EXACT_CODES if core.GEMV_EXACT_CODES else 0)   # what Linear4bit launches
+    alt_qt = prod_qt ^ _lib.EXACT_CODES
+    qt_flags = [prod_qt]
 
     def launch(i):
         p, qa, a2 = sets[i % copies]
@@ -266,13 +269,14 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(b2b)
     b2b_us = e0.elapsed_time(e1) * 1e3 / iters
-    # the same launches with exact (fp32) NF4 codes (QZ_EXACT_CODES: hi + lo fp16 code split)
-    qt_flags[0] = _lib.NF4 | _lib.EXACT_CODES
+    # the same launches with the other NF4 code precision (exact fp32 codes as hi + lo
+    # fp16 parts <-> fp16-rounded codes)
+    qt_flags[0] = alt_qt
     for i in range(copies):
         launch(i)
     blocked(b2b)
-    exact_us = e0.elapsed_time(e1) * 1e3 / iters
-    qt_flags[0] = _lib.NF4
+    alt_us = e0.elapsed_time(e1) * 1e3 / iters
+    qt_flags[0] = prod_qt
     # one-shot read floor of the same 8.39 MB packed weight (same rotation, same timing method)
     sink = torch.zeros(1, dtype=torch.int32, device=dev)
     floor_fn = _lib.lib.qz_bench_read_floor
@@ -303,7 +307,8 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(empty)
     empty_us = e0.elapsed_time(e1) * 1e3 / iters
-    GEMV_EXTRA["exact_codes_launch_us"] = round(exact_us, 3)
+    GEMV_EXTRA["codes"] = "exact (fp32 as hi+lo fp16)" if prod_qt & _lib.EXACT_CODES else "fp16"
+    GEMV_EXTRA["other_codes_launch_us"] = round(alt_us, 3)
     return statistics.mean(us), statistics.median(us), b2b_us, floor_us, empty_us
 
 
@@ -695,7 +700,7 @@ def main():
                 "empty_launch_us": round(empty_us, 3),
                 "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
                                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "exact_codes_launch_us": GEMV_EXTRA.get("exact_codes_launch_us"),
+                "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline()}
         parity = gemv_parity()
 

@@ -504,6 +504,341 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
   }
 }
 
+// Large-T prefill, staggered two-group schedule ("8-phase"; guide section 5 template,
+// re-derived for a W operand that is DECODED into LDS, not copied):
+//   * same 256 x 256 tile, 8 waves as 2 (tokens: wave group g = wave >> 2) x 4
+//     (rows), 128 tokens x 64 rows per wave, K-step 64 = one scale block per row,
+//     same LDS images / swizzle / epilogue as k_gemm_4bit_big;
+//   * a K-step is 4 phases, one C quadrant (64 tokens x 32 rows = 16 MFMAs) each.
+//     A phase is [read segment] s_barrier [16 MFMAs] s_barrier; group 1 starts one
+//     barrier late, so in every barrier interval one group runs MFMAs while the
+//     other (the wave on the same SIMD) issues its fragment ds_reads, its share of
+//     the next step's W decode and its staging DMAs -- the decode's VALU and the
+//     LDS traffic hide under the other group's matrix work;
+//   * quadrant order (rows lo, tok lo), (rows hi, tok lo), (rows hi, tok hi),
+//     (rows lo, tok hi): each phase loads only the fragments that change
+//     (12, 4, 8, 4 ds_read_b128);
+//   * staging (all LDS DMA, issued in phase 0 of step s): X(s+1) into the other X
+//     buffer (free: every wave passed its last read of step s-1 one barrier
+//     earlier) and the packed bytes + scales of W(s+2) into a 2-slot ring; phase
+//     3 of step s retires them with vmcnt(0) before its barrier, so step s+1 reads
+//     them after >= 1 barrier (the RAW rule of the guide);
+//   * W(s+1) is decoded during step s, one packed dword (8 codes -> 16 B of the
+//     exact fp16/bf16 image) per thread per phase, into the other W buffer; the
+//     per-(row, block) table is built in phase 0.  Phase 3 waits lgkmcnt(0) before
+//     its barrier, so the image is complete before any wave reads it.
+// V (microbenchmark A/B, timing only except 0 and 2): 0 = product; 1 = no decode
+// (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
+// 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone).
+#ifdef QZ_STAMPS8P
+__device__ unsigned long long g_qz_stamp8p[2 * 8 * 16];
+#endif
+// scheduling hint for one MFMA segment: 16 x {1 MFMA, N VALU} (the decode's VALU goes into the
+// issue slots the MFMAs leave free instead of queueing after the last one)
+template <int N> __device__ __forceinline__ void interleave_mfma_valu() {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, N, 0);
+  }
+}
+constexpr int k8pX = 0, k8pW = 2 * kBigStage, k8pWp = 4 * kBigStage, k8pSc = k8pWp + 2 * kBigWp;
+constexpr int k8pCode2 = k8pSc + 2 * 2048;
+template <int QT, bool DQ, int DT, int V = 0>
+__global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[k8pCode2 + (DQ ? 1024 : 0)];
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  typedef __attribute__((address_space(1))) void *glb_ptr_t;
+  float *s_code2 = reinterpret_cast<float *>(smem + k8pCode2);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 2, wm = wave & 3;
+
+  // XCD-aware, bijective tile order (as k_gemm_4bit_big)
+  const int tiles_m = (p.M + kBigM - 1) / kBigM;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (wg % tiles_m) * kBigM, t0 = (wg / tiles_m) * kBigT;
+  const int nsteps = p.K / kBK;
+
+  // ---- staging (LDS DMA only) ----
+  const unsigned char *xbase = reinterpret_cast<const unsigned char *>(p.X);
+  uint32_t xoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (8 * i + wave) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    xoff[i] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * chunk) * 2u;
+  }
+  // instruction i of every wave stages token quarter i (rows 64 i .. 64 i + 63 of the tile)
+  auto stage_xq = [&](int step, int buf, int i) {
+    if constexpr (V >= 4) return;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(xbase + xoff[i] + (uint32_t)step * (kBK * 2)),
+                                     (lds_ptr_t)(smem + k8pX + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
+  };
+  const int wr = tid >> 1, wh = tid & 1;  // decode ownership: row wr, 32-code half wh
+  const int wrow = min(m0 + wr, p.M - 1);
+  const unsigned char *wptr = p.B + (size_t)wrow * ((uint32_t)p.K >> 1) + 16 * wh;
+  const uint32_t blk_row = (uint32_t)(((long long)wrow * p.K) >> p.bs_log2);
+  const int srow = tid & 255;
+  const uint32_t blk_row_s = (uint32_t)(((long long)min(m0 + srow, p.M - 1) * p.K) >> p.bs_log2);
+  auto dma_w = [&](int step, int slot) {
+    if constexpr (V >= 3) return;
+    const int k0 = step * kBK;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(wptr + (k0 >> 1)),
+                                     (lds_ptr_t)(smem + k8pWp + slot * kBigWp + wave * 1024), 16, 0, 0);
+    const uint32_t b = blk_row_s + ((uint32_t)k0 >> p.bs_log2);
+    const void *src;
+    if constexpr (DQ)
+      src = tid < 256 ? (const void *)(p.sc.qabsmax + (b & ~3u)) : (const void *)(p.sc.absmax2 + (b >> p.bs2_log2));
+    else
+      src = p.sc.absmax + b;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)src, (lds_ptr_t)(smem + k8pSc + slot * 2048 + wave * 256), 4, 0, 0);
+  };
+  float offset = 0.0f;
+  // the exact per-(row, block) table of step `step` (its packed bytes + scales sit in `slot`):
+  // read_scale issues the LDS reads (ahead of the phase's fragment reads), make_table the VALU
+  struct ScaleWords {
+    uint32_t q;
+    float a;
+  };
+  auto read_scale = [&](int slot) {
+    const unsigned char *sc = smem + k8pSc + slot * 2048;
+    return ScaleWords{DQ ? *reinterpret_cast<const uint32_t *>(sc + wr * 4) : 0u,
+                      *reinterpret_cast<const float *>(sc + 1024 + wr * 4)};
+  };
+  auto make_table = [&](int step, const ScaleWords &sw, uint32_t (&t)[8]) {
+    float am;
+    if constexpr (DQ) {
+      const uint32_t b = blk_row + ((uint32_t)(step * kBK) >> p.bs_log2);
+      const uint32_t q = (sw.q >> (8 * (b & 3))) & 255u;
+      am = __fadd_rn(__fmul_rn(s_code2[q], sw.a), offset);   // core.py:467-468
+    } else {
+      am = sw.a;
+    }
+    block_table<QT, DT>(am, t);
+  };
+  auto read_packed = [&](int slot, int d) {
+    return *reinterpret_cast<const uint32_t *>(smem + k8pWp + slot * kBigWp + tid * 16 + 4 * d);
+  };
+  // packed dword d of this thread's 16 bytes -> 8 exact 16-bit weights -> W image chunk 4 wh + d
+  auto decode_dword = [&](uint32_t w, int buf, int d, const uint32_t (&t)[8]) {
+    unsigned char *dst = smem + k8pW + buf * kBigStage + lds_off(wr, 4 * wh + d);
+    if constexpr (V == 1 || V == 3 || V == 4) {
+      *reinterpret_cast<v4u *>(dst) = v4u{w, w ^ t[0], w, w};
+    } else {
+      uint32_t N[4];
+      decode_codes_natural(w, t, N);
+      *reinterpret_cast<v4u *>(dst) = v4u{N[0], N[1], N[2], N[3]};
+    }
+  };
+
+  // ---- fragments (as k_gemm_4bit_big: one lane offset per k-half) ----
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t frag_lane[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                                 (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  f4_t acc[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+  v4u xf[2][4];  // X fragments of the current token half: [kk][i]
+  v4u wf[2][2];  // W fragments of the current row half: [kk][j]
+  auto load_x = [&](int buf, int th) {
+    const unsigned char *sx = smem + k8pX + buf * kBigStage + (128 * wt + 64 * th) * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xf[kk][i] = *reinterpret_cast<const v4u *>(sx + frag_lane[kk] + 16 * i * 128);
+  };
+  auto load_w = [&](int buf, int rh) {
+    const unsigned char *sw = smem + k8pW + buf * kBigStage + (64 * wm + 32 * rh) * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[kk][j] = *reinterpret_cast<const v4u *>(sw + frag_lane[kk] + 16 * j * 128);
+  };
+  auto mfma_quadrant = [&](int rh, int th) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f4_t &c = acc[2 * rh + j][4 * th + i];
+          if constexpr (DT == QZ_DT_F16)
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, wf[kk][j]),
+                                                       __builtin_bit_cast(h8_t, xf[kk][i]), c, 0, 0, 0);
+          else
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, wf[kk][j]),
+                                                        __builtin_bit_cast(b8_t, xf[kk][i]), c, 0, 0, 0);
+        }
+  };
+
+  // ---- prologue: X(0), X(1), W(0) and W(1) staged; W(0) decoded ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) stage_xq(0, 0, i);
+  dma_w(0, 0);
+  if (nsteps > 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stage_xq(1, 1, i);
+    dma_w(1, 1);
+  }
+  if constexpr (DQ) {
+    if (tid < 256) s_code2[tid] = p.sc.code2[tid];
+    offset = *p.sc.offset;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  {
+    uint32_t t[8];
+    make_table(0, read_scale(0), t);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) decode_dword(read_packed(0, d), 0, d, t);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  if (V != 2 && wt == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier interval behind
+#ifdef QZ_STAMPS8P
+  unsigned long long st8[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define QZ_ST8(k)                                                                       \
+  do {                                                                                \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                     \
+    st8[k] = s == 10 ? now_ : st8[k];                                                 \
+  } while (0)
+#else
+#define QZ_ST8(k) do {} while (0)
+#endif
+  // A phase: [read segment: LDS reads + DMA issue only, no waits] s_barrier [lgkmcnt(0);
+  // 16 MFMAs with this phase's share of the W(s+1) decode interleaved] s_barrier.
+  for (int s = 0; s < nsteps; ++s) {
+    const int b = s & 1;
+    const bool dma = s + 2 < nsteps;    // stage X(s+2) (into this step's buffer, quarter by quarter as
+                                        // its last reader passes) and W(s+2)'s packed bytes + scales
+    const int ps = (s + 1) & 1;         // ring slot of W(s+1)'s packed bytes
+    uint32_t t[8], w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    ScaleWords sw{0u, 0.0f};
+    QZ_ST8(0);
+    // ---------------- phase 0: quadrant (rows lo, tokens lo) ----------------
+    // decode inputs are read unconditionally: in the last step they are stale ring bytes, decoded
+    // into the idle W buffer and never read (keeps the MFMA segments straight-line, so the
+    // decode VALU interleaves with the MFMAs)
+    sw = read_scale(ps);
+    w0 = read_packed(ps, 0);
+    if constexpr (V >= 3) sw.q = sw.q & 0u;
+    load_w(b, 0);
+    load_x(b, 0);
+    if (dma) dma_w(s + 2, s & 1);
+    __builtin_amdgcn_s_barrier();
+    QZ_ST8(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quadrant(0, 0);
+    make_table(s + 1, sw, t);
+    decode_dword(w0, b ^ 1, 0, t);
+    interleave_mfma_valu<4>();
+    __builtin_amdgcn_s_setprio(0);
+    QZ_ST8(2);
+    __builtin_amdgcn_s_barrier();
+    // ---------------- phase 1: (rows hi, tokens lo) ----------------
+    w1 = read_packed(ps, 1);
+    w2 = read_packed(ps, 2);
+    load_w(b, 1);
+    if (dma) {  // quarters 0 (group 0, tokens lo) and 2 (group 1, tokens lo): last read in phase 0
+      stage_xq(s + 2, b, 0);
+      stage_xq(s + 2, b, 2);
+    }
+    __builtin_amdgcn_s_barrier();
+    QZ_ST8(3);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quadrant(1, 0);
+    decode_dword(w1, b ^ 1, 1, t);
+    decode_dword(w2, b ^ 1, 2, t);
+    interleave_mfma_valu<4>();
+    __builtin_amdgcn_s_setprio(0);
+    QZ_ST8(4);
+    __builtin_amdgcn_s_barrier();
+    // ---------------- phase 2: (rows hi, tokens hi) ----------------
+    w3 = read_packed(ps, 3);
+    load_x(b, 1);
+    __builtin_amdgcn_s_barrier();
+    QZ_ST8(5);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quadrant(1, 1);
+    decode_dword(w3, b ^ 1, 3, t);
+    interleave_mfma_valu<2>();
+    __builtin_amdgcn_s_setprio(0);
+    // the W(s+1) image is complete: every wave's stores retired before this barrier (>= 3
+    // barriers before step s+1's first read of it)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    QZ_ST8(6);
+    __builtin_amdgcn_s_barrier();
+    // ---------------- phase 3: (rows lo, tokens hi); retire the step's staging ----------------
+    load_w(b, 0);
+    if (dma) {  // quarters 1 and 3 (tokens hi): last read in phase 2
+      stage_xq(s + 2, b, 1);
+      stage_xq(s + 2, b, 3);
+    }
+    // retire X(s+1) and W(s+2)'s bytes; X(s+2)'s four quarter DMAs may stay in flight
+    if (dma) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    QZ_ST8(7);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_quadrant(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    QZ_ST8(8);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (V != 2 && wt == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
+#ifdef QZ_STAMPS8P
+  if (V == 0 && lane == 0 && nsteps > 10 && (blockIdx.x == 0 || blockIdx.x == 100)) {
+    for (int k = 0; k < 9; ++k) g_qz_stamp8p[((blockIdx.x ? 1 : 0) * 8 + wave) * 16 + k] = st8[k];
+  }
+#endif
+
+  // ---- epilogue (as k_gemm_4bit_big): lane holds weight rows 16j + 4fk + r of token 16i + fr ----
+  __syncthreads();
+  unsigned char *ew = smem + wave * (64 * kBigERow);
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = min(m0 + 64 * wm + 16 * j + 4 * fk + r, p.M - 1);
+      bv[j][r] = p.bias ? load_f32<DT>(p.bias, m) : 0.0f;
+    }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4_t v = acc[j][4 * h + i];
+        const uint32_t lo = cvt_pk16<DT>(v[0] + bv[j][0], v[1] + bv[j][1]);
+        const uint32_t hi = cvt_pk16<DT>(v[2] + bv[j][2], v[3] + bv[j][3]);
+        *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * kBigERow + (16 * j + 4 * fk) * 2) = uint2{lo, hi};
+      }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int qd = lane + 64 * it, tok = qd >> 3, c16 = qd & 7;
+      const v4u v = *reinterpret_cast<const v4u *>(ew + tok * kBigERow + c16 * 16);
+      const int t = t0 + 128 * wt + 64 * h + tok, m = m0 + 64 * wm + 8 * c16;
+      if (t < p.T && m < p.M)
+        *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
+    }
+  }
+}
+
 // Multi-token GEMV for 2 <= T <= 16 (small-batch decode, short prefills).
 // A 512-thread workgroup owns 16 weight rows; its 8 waves split K and meet in
 // LDS (no workspace, no second launch).  Per 256-element chunk, lane
@@ -806,7 +1141,7 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
     p.ws = nullptr;
     p.k_split = K;
     const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
-#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_big<QT_, DQ_, DT_, 3>), dim3(g), dim3(512), 0, s, p)
+#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_8p<QT_, DQ_, DT_, 0>), dim3(g), dim3(512), 0, s, p)
 #define QZ_BIG_DT(QT_, DQ_) \
   do { if (dtype == QZ_DT_F16) QZ_BIG(QT_, DQ_, QZ_DT_F16); else QZ_BIG(QT_, DQ_, QZ_DT_BF16); } while (0)
     if (quant_type == QZ_FP4) {

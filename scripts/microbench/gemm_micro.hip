@@ -1,6 +1,9 @@
 // Dev microbenchmark (not shipped): prefill GEMM kernels on a 4096x4096 (or
 // M x K) NF4 + double-quant weight: the 128-row tile kernel (k_gemm_4bit) vs
 // the 256x256 tile kernel (k_gemm_4bit_big), random operands, stream parked.
+#ifdef STAMPS
+#define QZ_STAMPS8P
+#endif
 #include "../../quantizations_amd/csrc/gemm.hip"
 
 #include <cstdio>
@@ -48,14 +51,17 @@ int main(int argc, char **argv) {
   p.bias = nullptr;
   struct V { std::string n; int T; std::function<void()> f; std::vector<double> us; };
   std::vector<V> vs;
-  const int Ts[] = {1024, 4096, 16384};
+  const int Ts[] = {4096, 16384};
   for (int T : Ts) {
     vs.push_back({"old128 T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T;
       hipLaunchKernelGGL((k_gemm_4bit<QZ_NF4, true, QZ_DT_F16, 128>), dim3((M + 127) / 128, (T + 127) / 128, 1), dim3(256), 0, 0, q); }, {}});
 #define BIGV(V_) vs.push_back({"big256 V=" #V_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
       const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
       hipLaunchKernelGGL((k_gemm_4bit_big<QZ_NF4, true, QZ_DT_F16, V_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { BIGV(3); BIGV(4); }
+#define P8V(V_) vs.push_back({"8phase V=" #V_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
+      const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
+      hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, V_>), dim3(g), dim3(512), 0, 0, q); }, {}})
+    if (T >= 4096) { BIGV(3); P8V(0); P8V(1); P8V(2); P8V(3); P8V(4); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());
@@ -71,6 +77,20 @@ int main(int argc, char **argv) {
       v.us.push_back(ms * 1e3 / it);
     }
   printf("M=%d K=%d NF4+DQ f16, random operands\n", M, K);
+#ifdef STAMPS
+  {
+    unsigned long long h[2 * 8 * 16];
+    CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_qz_stamp8p), sizeof(h)));
+    printf("stamps (step 10, shader clocks rel. to wave 0's first stamp): per phase [read-seg, wait barrier1, mfma, wait barrier2]\n");
+    for (int wgi = 0; wgi < 2; ++wgi)
+      for (int w = 0; w < 8; ++w) {
+        const unsigned long long *q = h + (wgi * 8 + w) * 16, base = h[wgi * 8 * 16];
+        printf("wg%d w%d:", wgi, w);
+        for (int k = 0; k < 9; ++k) printf(" %6lld", (long long)(q[k] - base));
+        printf("\n");
+      }
+  }
+#endif
   for (auto &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const double med = v.us[v.us.size() / 2];

@@ -690,7 +690,8 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_gemv_4bit<Tab,DQ,f16,R=2,WK=1> 4096x4096 NF4+DQ (LDS byte-table decode)",
+                "kernel": "k_gemv_4bit<Tab,DQ,f16,R=2,WK=1,full-step,CL=%d> 4096x4096 NF4+DQ (LDS byte-table decode, "
+                          "%s codes)" % (int(GEMV_EXTRA.get("codes", "").startswith("exact")), GEMV_EXTRA.get("codes")),
                 "launch_us_avg": round(b2b_us, 3),
                 "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
                 "one_shot_read_floor_us": round(floor_us, 3),

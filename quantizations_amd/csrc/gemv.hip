@@ -785,7 +785,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
         if (row < p.M) {
           float o = v[r] * out_scale;
           if (p.bias) o += load_f32<DT>(p.bias, row);
-          store_f32<DT>(p.y, row, o);
+          if constexpr ((ABL & 1024) != 0 && DT == QZ_DT_F16)  // microbenchmark: non-temporal y store
+            __builtin_nontemporal_store((uint16_t)f32_to_f16_bits(o), reinterpret_cast<uint16_t *>(p.y) + row);
+          else
+            store_f32<DT>(p.y, row, o);
         }
       }
     }

@@ -121,6 +121,21 @@ __global__ __launch_bounds__(T) void k_read_floor_store(const unsigned char *__r
   if ((threadIdx.x & 63) < 2) out[(blockIdx.x * T + threadIdx.x) / 32] = acc;  // 2 rows' worth per wave
 }
 
+template <int T, int L>
+__global__ __launch_bounds__(T) void k_read_floor_store_nt(const unsigned char *__restrict__ p, long long bytes, uint32_t *out) {
+  const long long nchunk = bytes / 16;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const long long c = ((long long)blockIdx.x * L + i) * T + threadIdx.x;
+    if (c < nchunk) {
+      v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p) + c);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  if ((threadIdx.x & 63) < 2) __builtin_nontemporal_store(acc, out + (blockIdx.x * T + threadIdx.x) / 32);
+}
+
 // one-shot floor with timeline stamps (start, data back, end) per wave
 __global__ __launch_bounds__(256) void k_floor_stamp(const unsigned char *__restrict__ p, long long bytes, uint32_t *sink) {
   unsigned long long t0, t1;
@@ -271,6 +286,17 @@ int main(int argc, char **argv) {
     GVF(3, true, 2, 1, 4, false, 0); GVF(3, true, 2, 1, 4, false, 256);
     GVS(3, true, 2, 1, 4);
   }
+  const bool cl = argc > 4 && std::string(argv[4]) == "cl";
+#define GVC(R, ABL, CL_) timeit("gemvFS tab dq R=" #R " ABL=" #ABL " CL=" #CL_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, ABL, true, CL_>), dim3(g), dim3(256), 0, 0, q); })
+  if (cl) {  // exact-code (CL) table vs fp16 codes; non-temporal y stores; store drain on the floor kernel
+    timeit("floor+store-nt T=256 L=2", [&](int i) { const long long nchunk = pbytes / 16;
+      const unsigned g = (unsigned)((nchunk + 511) / 512);
+      hipLaunchKernelGGL((k_read_floor_store_nt<256, 2>), dim3(g), dim3(256), 0, 0, P[i % NC], (long long)pbytes, fout); });
+    GVC(2, 0, false); GVC(2, 0, true); GVC(2, 1024, false); GVC(2, 1024, true); GVC(4, 0, true); GVC(1, 0, true);
+  }
   const bool tabab2 = argc > 4 && std::string(argv[4]) == "tabab2";
 #define GVFS(R, ABL) timeit("gemvFS tab dq R=" #R " ABL=" #ABL, [&, pt = p](int i) { \
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
@@ -300,7 +326,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

@@ -715,7 +715,11 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "decode tokens/sec Llama-3-8B NF4 bs=1; 4096×4096 GEMV GB/s vs HBM peak",
+            # BASELINE.json's metric for the headline model; other configs name their own model/codebook
+            "metric": ("decode tokens/sec Llama-3-8B NF4 bs=1; 4096×4096 GEMV GB/s vs HBM peak"
+                       if (args.model, args.quant) == ("llama3-8b", "nf4") else
+                       f"decode tokens/sec {'Llama-3-70B' if args.model == 'llama3-70b' else 'Llama-3-8B'} "
+                       f"{args.quant.upper()} bs=1; 4096×4096 GEMV GB/s vs HBM peak"),
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",

@@ -297,6 +297,15 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL((k_read_floor_store_nt<256, 2>), dim3(g), dim3(256), 0, 0, P[i % NC], (long long)pbytes, fout); });
     GVC(2, 0, false); GVC(2, 0, true); GVC(2, 1024, false); GVC(2, 1024, true); GVC(4, 0, true); GVC(1, 0, true);
   }
+  const bool clsweep = argc > 4 && std::string(argv[4]) == "clsweep";
+#define GVCS(R, WK, NW) timeit("gemvFS CL R=" #R " WK=" #WK " NW=" #NW, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, WK, NW, false, 0, true, true>), dim3(g), dim3(NW * 64), 0, 0, q); })
+  if (clsweep) {  // exact-code full-step kernel: waves per workgroup, rows per wave, K split
+    GVCS(2, 1, 4); GVCS(2, 2, 4); GVCS(1, 2, 4); GVCS(1, 1, 4); GVCS(4, 1, 4); GVCS(4, 2, 4);
+    GVCS(2, 1, 8); GVCS(2, 2, 8); GVCS(1, 2, 8); GVCS(4, 2, 8); GVCS(2, 4, 8); GVCS(1, 4, 4);
+  }
   const bool tabab2 = argc > 4 && std::string(argv[4]) == "tabab2";
 #define GVFS(R, ABL) timeit("gemvFS tab dq R=" #R " ABL=" #ABL, [&, pt = p](int i) { \
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
@@ -326,7 +335,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
@@ -400,6 +409,9 @@ int main(int argc, char **argv) {
       run("gemv tab DQ R=2 full-step", g * 4, [&, pt = p](int i) {
         GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC];
         hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true>), dim3(g), dim3(256), 0, 0, q); });
+      run("gemv tab DQ R=2 full-step exact codes (product)", g * 4, [&, pt = p](int i) {
+        GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
+        hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true>), dim3(g), dim3(256), 0, 0, q); });
     }
     return 0;
   }

@@ -225,7 +225,8 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
     fn = _lib.lib.qz_gemv_4bit
 
     from quantizations_amd import core
-    prod_qt = _lib.NF4 | (_lib.EXACT_CODES if core.GEMV_EXACT_CODES else 0)   # what Linear4bit launches
+    # what Linear4bit launches for fp16 activations
+    prod_qt = core._gemv_quant_type("nf4", None, torch.float16)
     alt_qt = prod_qt ^ _lib.EXACT_CODES
     qt_flags = [prod_qt]
 
@@ -324,6 +325,7 @@ def gemv_parity():
     default fp16-code table and the exact-code variant; fp16 output (the bench
     config) and fp32 output (x in fp32: the code error is not hidden by the
     output rounding)."""
+    from quantizations_amd import _lib
     from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
 
     dev = torch.device("cuda")
@@ -344,13 +346,12 @@ def gemv_parity():
                     float(f"{((y - ref).norm() / ref.norm()).item():.3e}")
         res[f"{M}x{K}"] = row
         del wd, packed, st
-    return {"rel_err_vs_fp32_weight_products": res, "tolerance": 1e-3,
-            "default": "exact_codes" if _exact_default() else "fp16_codes"}
-
-
-def _exact_default() -> bool:
     from quantizations_amd import core
-    return core.GEMV_EXACT_CODES
+    return {"rel_err_vs_fp32_weight_products": res, "tolerance": 1e-3,
+            "default": {"f16_activations": "exact_codes" if core._gemv_quant_type("nf4", None, torch.float16)
+                        & _lib.EXACT_CODES else "fp16_codes",
+                        "f32_activations": "exact_codes" if core._gemv_quant_type("nf4", None, torch.float32)
+                        & _lib.EXACT_CODES else "fp16_codes"}}
 
 
 def gemv_alg_bytes(shapes, dq: bool = True, x_bytes: int = 2, y_bytes: int = 2) -> int:

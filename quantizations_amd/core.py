@@ -362,17 +362,23 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, blocksi
     return out.t()
 
 
-# Decode GEMV codebook precision.  The reference GEMV multiplies by its fp32
-# quant_map (kernels.cu:1115-1120).  The default byte-table decode holds the
-# NF4 codes as fp16 (<= 2.4e-4 relative per code); exact codes
-# split each fp32 code into two fp16 parts (~2^-23 relative: fp32-class) at the
-# cost of one more dot product per weight pair.  FP4 is exact either way.
-GEMV_EXACT_CODES = os.environ.get("QZ_GEMV_EXACT_CODES", "1") == "1"
+# Decode GEMV codebook precision.  The reference's only exported GEMV takes fp32
+# activations and multiplies by its fp32 quant_map (kernels.cu:1115-1120); bnb's
+# fp16 GEMV holds the codebook in the activation type.  The byte-table decode
+# either holds the codes as fp16 (<= 2.4e-4 relative per NF4 code) or, with exact
+# codes, splits each fp32 code into two fp16 parts (~2^-23: fp32-class) at the cost
+# of one more dot product per weight pair (+3 % at 4096^2, +13 % on the grouped
+# gate/up launch).  "auto" (default): exact codes for fp32
+# activations -- the reference's numerics -- and fp16 codes for fp16/bf16
+# activations, whose output rounding (2^-11 / 2^-8) is as large as the code
+# rounding.  FP4 is exact either way; a runtime LUT always decodes exactly.
+GEMV_EXACT_CODES = os.environ.get("QZ_GEMV_EXACT_CODES", "auto")   # "auto" | "1" | "0"
 
 
-def _gemv_quant_type(quant_type: str, exact_codes: Optional[bool]) -> int:
-    exact = GEMV_EXACT_CODES if exact_codes is None else exact_codes
-    return _lib.QUANT_TYPES[quant_type] | (_lib.EXACT_CODES if exact else 0)
+def _gemv_quant_type(quant_type: str, exact_codes: Optional[bool], dtype: torch.dtype) -> int:
+    if exact_codes is None:
+        exact_codes = dtype == torch.float32 if GEMV_EXACT_CODES == "auto" else GEMV_EXACT_CODES == "1"
+    return _lib.QUANT_TYPES[quant_type] | (_lib.EXACT_CODES if exact_codes else 0)
 
 
 def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
@@ -380,7 +386,8 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
               exact_codes: Optional[bool] = None) -> Tensor:
     """Batch-1 4-bit GEMV (reference core.py:426-504) as ONE fused kernel:
     y = x . W^T (+ bias), W from `state`; out dtype = A.dtype.  `exact_codes`
-    (default GEMV_EXACT_CODES) decodes with the fp32 codebook values."""
+    (default: GEMV_EXACT_CODES, "auto" = exact for fp32 activations) decodes with
+    the fp32 codebook values."""
     if state is None:
         raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
     if A.numel() != A.shape[-1]:
@@ -395,7 +402,7 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     A = A.contiguous()
     if bias is not None and bias.dtype != A.dtype:
         bias = bias.to(A.dtype)
-    check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _gemv_quant_type(state.quant_type, exact_codes),
+    check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _gemv_quant_type(state.quant_type, exact_codes, A.dtype),
                            state.blocksize, *state.scale_args(), block_base, 0, ptr(bias), ptr(out),
                            _lib.stream_of(A)), "gemv_4bit")
     return out
@@ -440,7 +447,7 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
         outs.append(y)
     bs2 = int(s0.state2.blocksize) if s0.nested else 0
     check(lib.qz_gemv_4bit_grouped(len(items), ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
-                                   _gemv_quant_type(s0.quant_type, exact_codes), s0.blocksize, bs2, 0,
+                                   _gemv_quant_type(s0.quant_type, exact_codes, A.dtype), s0.blocksize, bs2, 0,
                                    _lib.stream_of(A)),
           "gemv_4bit_grouped")
     return outs

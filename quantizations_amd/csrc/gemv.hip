@@ -401,7 +401,7 @@ __device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)
 // byte value, so the address of byte m is (byte << 7) | jb either way.
 // (ABL: benchmark-only ablations -- 16 replaces the dot products by integer
 // adds, 32 replaces the table reads by the addresses themselves.)
-template <bool SPLIT, int ABL = 0, bool CL = false>
+template <bool SPLIT, int ABL = 0, bool CL = false, bool WT = false>
 __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&hi)[16],
                                                const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t *s_tab,
                                                uint32_t jb) {
@@ -410,9 +410,18 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
   uint32_t v[16], vl[CL ? 16 : 1];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    // byte m of w, times 128 (the stride of one entry), plus the copy
-    const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
-                           ((w[d] >> 9) & 0x7F80u) | jb, ((w[d] >> 17) & 0x7F80u) | jb};
+    // byte m of w, times the stride of one entry (128 B; WT: 256 B), plus the copy.  WT builds
+    // the address with ONE v_perm: byte 0 = the lane's copy offset jb (< 256), byte 1 = byte m
+    uint32_t a[4];
+    if constexpr (WT) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = __builtin_amdgcn_perm(w[d], jb, 0x0C0C0000u | ((4u + m) << 8));
+    } else {
+      a[0] = ((w[d] << 7) & 0x7F80u) | jb;
+      a[1] = ((w[d] >> 1) & 0x7F80u) | jb;
+      a[2] = ((w[d] >> 9) & 0x7F80u) | jb;
+      a[3] = ((w[d] >> 17) & 0x7F80u) | jb;
+    }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       if constexpr ((ABL & 32) != 0) {
@@ -465,7 +474,7 @@ __device__ __forceinline__ float wave_sum_last(float v) {
 
 // Builds the kModeTab byte table from the 16-entry fp16 byte planes t[8]
 // (every thread of the workgroup takes part; the caller synchronises).
-template <int NT>
+template <int NT, int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t (&t)[8]) {
   for (int e = threadIdx.x; e < 256; e += NT) {
     uint32_t P[4];
@@ -475,9 +484,9 @@ __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t
     // 128 B per entry; rotate the 16-B pieces by lane so that each 8-lane
     // store group covers all 32 banks
 #pragma unroll
-    for (int i = 0; i < kTabCopies / 4; ++i) {
-      const int piece = (i + (int)threadIdx.x) & (kTabCopies / 4 - 1);
-      reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = q;
+    for (int i = 0; i < PIECES; ++i) {
+      const int piece = (i + (int)threadIdx.x) & (PIECES - 1);
+      reinterpret_cast<u32x4 *>(s_tab)[e * PIECES + piece] = q;
     }
   }
 }
@@ -488,12 +497,13 @@ __device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t
 // 8-lane store group covers all 32 banks.  (Loading 8 pieces per thread to
 // make every store address an immediate offset was measured slower: the
 // extra loads delay the first weight loads.)
+template <int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void store_byte_table_entry(uint32_t *s_tab, const u32x4 &v,
                                                        const uint32_t e = threadIdx.x) {
 #pragma unroll
-  for (int i = 0; i < kTabCopies / 4; ++i) {
-    const uint32_t piece = (e + (uint32_t)i) & (kTabCopies / 4 - 1);
-    reinterpret_cast<u32x4 *>(s_tab)[e * (kTabCopies / 4) + piece] = v;
+  for (int i = 0; i < PIECES; ++i) {
+    const uint32_t piece = (e + (uint32_t)i) & (PIECES - 1);
+    reinterpret_cast<u32x4 *>(s_tab)[e * PIECES + piece] = v;
   }
 }
 
@@ -511,7 +521,7 @@ __device__ __forceinline__ int lut_shift(const float *lut) {
 
 // Builds the CL (exact-code) byte table from a runtime fp32 codebook: entry
 // e = {hi pair, lo pair} of (code[e >> 4], code[e & 15]) * 2^S, 16 copies.
-template <int NT>
+template <int NT, int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const float *lut, int S) {
   for (int e = threadIdx.x; e < 256; e += NT) {
     const float ca = ldexpf(lut[e >> 4], S), cb = ldexpf(lut[e & 15], S);
@@ -519,7 +529,7 @@ __device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const fl
     const float ra = ca - (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu));
     const float rb = cb - (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
     const uint32_t l = cvt_pk_f16_rne(ra, rb);
-    store_byte_table_entry(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
+    store_byte_table_entry<PIECES>(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
   }
 }
 
@@ -606,8 +616,11 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
 };
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false>
+          bool CL = false, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
+  // WT ("wide table"): 256 B per byte value -- 64 copies of a 4-B entry, or 32 copies of an
+  // 8-B exact entry, 64 KiB -- so the lookup address is one v_perm and every copy is bank-private
+  constexpr int kPieces = WT ? 16 : kTabCopies / 4;
   static_assert(!CL || MODE == kModeTab, "exact codes need the byte-table decode");
   QZ_STAMP_DECL;
   QZ_STAMP(0);
@@ -617,7 +630,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ float s_part[NW][R];
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? kTabDwords : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? (WT ? 2 : 1) * kTabDwords : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -698,18 +711,19 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       if (p.lut) {
         const int S = lut_shift(p.lut);
         out_scale = ldexpf(1.0f, -S);
-        build_byte_table_exact<NW * 64>(s_tab, p.lut, S);
+        build_byte_table_exact<NW * 64, kPieces>(s_tab, p.lut, S);
       } else if (threadIdx.x < 256) {
-        store_byte_table_entry(s_tab, tab_entry);
+        store_byte_table_entry<kPieces>(s_tab, tab_entry);
       }
     } else {
-      if (p.lut) build_byte_table<NW * 64>(s_tab, t);
-      else if (threadIdx.x < 256) store_byte_table_entry(s_tab, tab_entry);
+      if (p.lut) build_byte_table<NW * 64, kPieces>(s_tab, t);
+      else if (threadIdx.x < 256) store_byte_table_entry<kPieces>(s_tab, tab_entry);
     }
   }
   if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
   QZ_STAMP(1);
-  const uint32_t jb = CL ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2;
+  const uint32_t jb = WT ? (CL ? (uint32_t)(lane & 31) << 3 : (uint32_t)lane << 2)
+                        : (CL ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2);
 
   float acc[R];
 #pragma unroll
@@ -733,7 +747,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       am = c.on ? am : 0.0f;
       if constexpr (kSplit) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
-      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, CL>(c.wv[r], hi, lo, s_tab, jb);
+      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, CL, WT>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
     }
@@ -817,9 +831,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false>
+          bool CL = false, bool WT = false>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT>(p, blockIdx.x);
 }
 
 // Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of

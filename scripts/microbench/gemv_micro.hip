@@ -302,6 +302,14 @@ int main(int argc, char **argv) {
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, WK, NW, false, 0, true, true>), dim3(g), dim3(NW * 64), 0, 0, q); })
+#define GVW(R, CL_, WT_) timeit("gemvFS R=" #R " CL=" #CL_ " WT=" #WT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, CL_, WT_>), dim3(g), dim3(256), 0, 0, q); })
+  const bool wt = argc > 4 && std::string(argv[4]) == "wt";
+  if (wt) {  // wide (256 B per entry) table: one v_perm per lookup address, bank-private copies
+    GVW(2, false, false); GVW(2, false, true); GVW(2, true, false); GVW(2, true, true); GVW(4, true, false); GVW(4, true, true);
+  }
   if (clsweep) {  // exact-code full-step kernel: waves per workgroup, rows per wave, K split
     GVCS(2, 1, 4); GVCS(2, 2, 4); GVCS(1, 2, 4); GVCS(1, 1, 4); GVCS(4, 1, 4); GVCS(4, 2, 4);
     GVCS(2, 1, 8); GVCS(2, 2, 8); GVCS(1, 2, 8); GVCS(4, 2, 8); GVCS(2, 4, 8); GVCS(1, 4, 4);
@@ -335,7 +343,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

@@ -591,14 +591,15 @@ def test_gemm_bias_and_batch_dims(orc):
 @pytest.mark.parametrize("qt", ["nf4", "fp4"])
 @pytest.mark.parametrize("dq", [True, False])
 @pytest.mark.parametrize("T,M,K", [(1, 256, 4096), (37, 512, 1024), (64, 4096, 4096), (200, 1024, 2048),
-                                   (4100, 520, 1024)])
+                                   (4100, 520, 1024), (4096, 264, 64), (4352, 256, 128)])
 def test_gemm_w_operand_is_the_dequantised_weight(qt, dq, dt, T, M, K):
     """One-hot activations read single weights back through the MFMA path: row t
     of Y must equal column k_t of dequantize_4bit(W, out_dtype=dt) BIT FOR BIT
     (values; -0.0 reads back as +0.0).  Pins the in-LDS decode (per-block
     fp16/bf16 table of code*absmax, double-quant rebuild, pair order shared by
     X and W) to the dequant kernel; covers both token tiles, split-K and (T >= 4096)
-    the 256 x 256 tile kernel with partial token and row tiles."""
+    the 256 x 256 tile kernel with partial token and row tiles, and its one- and two-step
+    K loops (K = 64, 128: no DMA two steps ahead, stale-ring decode of the last step)."""
     from quantizations_amd.core import dequantize_4bit, gemm_4bit, quantize_4bit
 
     W = _w(M, K, seed=3 * T + M)

@@ -429,11 +429,14 @@ def prefill_bench(T: int = 16384, iters: int = 10):
         def fused():
             return gemm_4bit(x, packed, qs, route="fused")
 
+        def own_route():
+            return gemm_4bit(x, packed, qs, route="gemm16")
+
         def ref_route():
             return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
 
         res = {}
-        for name, fn in (("fused", fused), ("dequant+hipblaslt", ref_route)):
+        for name, fn in (("fused", fused), ("dequant+gemm16_8phase", own_route), ("dequant+hipblaslt", ref_route)):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -446,11 +449,14 @@ def prefill_bench(T: int = 16384, iters: int = 10):
             res[name] = {"ms": round(ms, 3), "TFLOP/s": round(2.0 * T * M * K / (ms * 1e-3) / 1e12, 1)}
         out[f"{M}x{K}"] = res
         del W, packed, qs
-    from quantizations_amd.core import PREFILL_FUSED_MAX_TOKENS
+    from quantizations_amd.core import GEMM16_MIN_TILES, PREFILL_FUSED_MAX_TOKENS, PREFILL_GEMM16
     return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0,
-            "product_route": "fused" if T <= PREFILL_FUSED_MAX_TOKENS else "dequant+hipblaslt",
-            "note": "both routes multiply the same bit-exact dequantised weight; matmul_4bit takes the fused "
-                    f"MFMA kernel up to {PREFILL_FUSED_MAX_TOKENS} tokens (profiles/r1_prefill_mfma_util.txt)"}
+            "product_route": "fused" if T <= PREFILL_FUSED_MAX_TOKENS else
+                             ("dequant+gemm16_8phase" if PREFILL_GEMM16 else "dequant+hipblaslt"),
+            "note": "every route multiplies the same bit-exact dequantised weight; matmul_4bit takes the fused "
+                    f"MFMA kernel up to {PREFILL_FUSED_MAX_TOKENS} tokens, above it our dequant kernel + hipBLASLt "
+                    "(the reference's F.linear route) unless QZ_PREFILL_GEMM16=1 selects our 8-phase MFMA GEMM "
+                    f"(qz_gemm_16bit, >= {GEMM16_MIN_TILES} 256x256 tiles)"}
 
 
 @torch.inference_mode()
@@ -470,11 +476,14 @@ def prefill_sweep(Ts=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 1
         def fused():
             return gemm_4bit(x, packed, qs, route="fused")
 
+        def own_route():
+            return gemm_4bit(x, packed, qs, route="gemm16")
+
         def ref_route():
             return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
 
         row = {}
-        for name, fn in (("fused", fused), ("dequant+blas", ref_route)):
+        for name, fn in (("fused", fused), ("dequant+gemm16", own_route), ("dequant+blas", ref_route)):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -162,6 +162,17 @@ int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dtype, const u
 int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T, int K, const void *X, int ldx, int dtype,
                          int quant_type, int blocksize, int blocksize2, void *stream);
 
+/* Dense 16-bit GEMM Y[T,M] = X[T,K] . W[M,K]^T (+ bias), fp32 accumulation
+ * (v_mfma_f32_16x16x32_{f16,bf16}), on the same staggered 8-phase 256x256 schedule as the
+ * fused kernel.  The large-T prefill route: qz_dequantize_4bit (bit-exact 16-bit weight,
+ * kernels.cu:554-560) then this GEMM -- modules.py:62-64's "dequantise, then F.linear",
+ * both halves hand-written.  X/W/Y/bias share `dtype` (F16 or BF16); W is contiguous
+ * [M][K]; row strides in elements.  Requires qz_gemm_16bit_ok(...) (K % 64 == 0, M % 8 == 0,
+ * 16-B aligned X/W/Y, row strides % 8 == 0, 32-bit byte offsets), else QZ_ERR_SHAPE. */
+int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dtype, const void *W, const void *bias, void *Y,
+                  int ldy, void *stream);
+int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy);
+
 /* Workspace bytes qz_gemm_4bit uses for (T, M, K) at its preferred K split
  * (0 = no split). */
 long long qz_gemm_4bit_workspace_size(int T, int M, int K);

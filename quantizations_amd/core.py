@@ -455,11 +455,40 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
 
 # Prefill route (matmul_4bit with more than one token).  "fused": the MFMA
 # kernel qz_gemm_4bit (dequant in LDS, never in HBM); "dequant": the
-# reference's own route -- full-weight dequantize_4bit (our HIP kernel) then a
-# library GEMM (hipBLASLt).  "auto" takes the fused kernel up to
-# PREFILL_FUSED_MAX_TOKENS tokens (DESIGN.md section 5 has the measured
-# crossover) and the dequant route above it.
+# reference's own route (modules.py:62-64) -- full-weight dequantize_4bit (our
+# bit-exact HIP kernel) then the library GEMM (hipBLASLt), or, with
+# PREFILL_GEMM16 (env QZ_PREFILL_GEMM16=1) and >= GEMM16_MIN_TILES 256 x 256
+# output tiles, our staggered 8-phase MFMA GEMM (qz_gemm_16bit); "gemm16"
+# forces the latter where it applies.  "auto" takes the fused kernel up to
+# PREFILL_FUSED_MAX_TOKENS tokens and the dequant route above it (DESIGN.md
+# section 4.2 has the measured crossovers: hipBLASLt is 12-17 % faster than
+# qz_gemm_16bit at T >= 4096 today, so it stays the default).
 PREFILL_FUSED_MAX_TOKENS = int(os.environ.get("QZ_PREFILL_FUSED_MAX_T", "512"))
+PREFILL_GEMM16 = os.environ.get("QZ_PREFILL_GEMM16", "0") == "1"
+GEMM16_MIN_TILES = int(os.environ.get("QZ_GEMM16_MIN_TILES", "256"))
+
+
+def gemm_16bit(A: Tensor, W: Tensor, bias: Optional[Tensor] = None) -> Optional[Tensor]:
+    """Y = A . W^T (+ bias) on qz_gemm_16bit for fp16/bf16 A [..., K] and a contiguous
+    W [M, K] of the same dtype; None if the kernel does not take the shapes (the
+    caller then uses the library GEMM)."""
+    M, K = W.shape
+    lead = A.shape[:-1]
+    A2 = A.reshape(-1, K)
+    if A2.stride(-1) != 1 or A2.data_ptr() % 16 != 0:
+        A2 = A2.contiguous()
+    T = A2.shape[0]
+    if (A.dtype not in (torch.float16, torch.bfloat16) or W.dtype != A.dtype or not W.is_contiguous()
+            or (bias is not None and (bias.numel() != M or not bias.is_contiguous()))):
+        return None
+    out = torch.empty((T, M), dtype=A.dtype, device=A.device)
+    if not lib.qz_gemm_16bit_ok(T, M, K, ptr(A2), A2.stride(0), ptr(W), ptr(out), M):
+        return None
+    if bias is not None and bias.dtype != A.dtype:
+        bias = bias.to(A.dtype)
+    check(lib.qz_gemm_16bit(T, M, K, ptr(A2), A2.stride(0), dtype_code(A.dtype), ptr(W), ptr(bias), ptr(out), M,
+                            _lib.stream_of(A)), "gemm_16bit")
+    return out.reshape(*lead, M)
 
 
 def _gemm_fused_ok(A2: Tensor, state: QuantState, M: int, K: int) -> bool:
@@ -471,11 +500,14 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
     """Batched (prefill) 4-bit GEMM: A[..., K] . W^T (+ bias) -> [..., M].
 
     The fused MFMA kernel decodes W to exactly the values dequantize_4bit(B,
-    state, out_dtype=A.dtype) stores, so both routes multiply the same operand
-    and differ only in fp32 summation order (fp16/bf16 activations; other
-    dtypes take the dequant route)."""
-    if route not in ("auto", "fused", "dequant"):
-        raise ValueError(f"route must be 'auto', 'fused' or 'dequant', got {route!r}")
+    state, out_dtype=A.dtype) stores, so every route multiplies the same operand
+    and differs only in fp32 summation order (fp16/bf16 activations; other
+    dtypes take the dequant route).  route: "auto", "fused", "dequant" (dequant +
+    the library GEMM, or qz_gemm_16bit with PREFILL_GEMM16), "blas" (dequant +
+    the library GEMM, the reference's F.linear) or "gemm16" (dequant +
+    qz_gemm_16bit where it applies)."""
+    if route not in ("auto", "fused", "dequant", "blas", "gemm16"):
+        raise ValueError(f"route must be 'auto', 'fused', 'dequant', 'blas' or 'gemm16', got {route!r}")
     M, K = state.shape[0], state.shape[1]
     lead = A.shape[:-1]
     A2 = A.reshape(-1, K)
@@ -497,7 +529,12 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
                                ptr(out), M, ptr(ws), ws_bytes, _lib.stream_of(A)), "gemm_4bit")
         return out.reshape(*lead, M)
     cd = A.dtype if A.dtype in (torch.float16, torch.bfloat16) else None
-    W = dequantize_4bit(B, state, out_dtype=cd).t()
+    W = dequantize_4bit(B, state, out_dtype=cd).t()          # [M, K], contiguous
+    tiles = ((T + 255) // 256) * ((M + 255) // 256)
+    if cd is not None and (route == "gemm16" or (route != "blas" and PREFILL_GEMM16 and tiles >= GEMM16_MIN_TILES)):
+        Y = gemm_16bit(A, W, bias)
+        if Y is not None:
+            return Y
     return torch.nn.functional.linear(A, W.to(A.dtype), None if bias is None else bias.to(A.dtype))
 
 

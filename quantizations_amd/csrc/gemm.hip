@@ -527,9 +527,10 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 //     exact fp16/bf16 image) per thread per phase, into the other W buffer; the
 //     per-(row, block) table is built in phase 0.  Phase 3 waits lgkmcnt(0) before
 //     its barrier, so the image is complete before any wave reads it.
-// V (microbenchmark A/B, timing only except 0 and 2): 0 = product; 1 = no decode
+// V (microbenchmark A/B, timing only except 0, 2 and 5): 0 = product; 1 = no decode
 // (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
-// 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone).
+// 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone); 5 = a plain fp16 GEMM on the
+// same schedule (B = fp16 [M, K], staged by DMA like X; no decode).
 #ifdef QZ_STAMPS8P
 __device__ unsigned long long g_qz_stamp8p[2 * 8 * 16];
 #endif
@@ -542,6 +543,7 @@ template <int N> __device__ __forceinline__ void interleave_mfma_valu() {
     __builtin_amdgcn_sched_group_barrier(0x002, N, 0);
   }
 }
+constexpr int kPlainW = 5;  // k_gemm_4bit_8p variant: B is a dense 16-bit [M, K] weight (qz_gemm_16bit)
 constexpr int k8pX = 0, k8pW = 2 * kBigStage, k8pWp = 4 * kBigStage, k8pSc = k8pWp + 2 * kBigWp;
 constexpr int k8pCode2 = k8pSc + 2 * 2048;
 template <int QT, bool DQ, int DT, int V = 0>
@@ -573,9 +575,24 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   }
   // instruction i of every wave stages token quarter i (rows 64 i .. 64 i + 63 of the tile)
   auto stage_xq = [&](int step, int buf, int i) {
-    if constexpr (V >= 4) return;
+    if constexpr (V == 4) return;
     __builtin_amdgcn_global_load_lds((glb_ptr_t)(xbase + xoff[i] + (uint32_t)step * (kBK * 2)),
                                      (lds_ptr_t)(smem + k8pX + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
+  };
+  // V == kPlainW (qz_gemm_16bit): B is a dense 16-bit [M, K] weight staged by DMA like X, one
+  // step ahead into the other W buffer -- the schedule as a plain GEMM, no decode
+  uint32_t woff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (8 * i + wave) + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    woff[i] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * chunk) * 2u;
+  }
+  auto stage_wf = [&](int step, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + woff[i] + (uint32_t)step * (kBK * 2)),
+                                       (lds_ptr_t)(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
   };
   const int wr = tid >> 1, wh = tid & 1;  // decode ownership: row wr, 32-code half wh
   const int wrow = min(m0 + wr, p.M - 1);
@@ -584,7 +601,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   const int srow = tid & 255;
   const uint32_t blk_row_s = (uint32_t)(((long long)min(m0 + srow, p.M - 1) * p.K) >> p.bs_log2);
   auto dma_w = [&](int step, int slot) {
-    if constexpr (V >= 3) return;
+    if constexpr (V >= 3) return;  // (V 5 stages its fp16 W in stage_wf)
     const int k0 = step * kBK;
     __builtin_amdgcn_global_load_lds((glb_ptr_t)(wptr + (k0 >> 1)),
                                      (lds_ptr_t)(smem + k8pWp + slot * kBigWp + wave * 1024), 16, 0, 0);
@@ -624,6 +641,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   };
   // packed dword d of this thread's 16 bytes -> 8 exact 16-bit weights -> W image chunk 4 wh + d
   auto decode_dword = [&](uint32_t w, int buf, int d, const uint32_t (&t)[8]) {
+    if constexpr (V == kPlainW) return;
     unsigned char *dst = smem + k8pW + buf * kBigStage + lds_off(wr, 4 * wh + d);
     if constexpr (V == 1 || V == 3 || V == 4) {
       *reinterpret_cast<v4u *>(dst) = v4u{w, w ^ t[0], w, w};
@@ -691,7 +709,10 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  {
+  if constexpr (V == kPlainW) {
+    stage_wf(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
     uint32_t t[8];
     make_table(0, read_scale(0), t);
 #pragma unroll
@@ -725,27 +746,35 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     // decode inputs are read unconditionally: in the last step they are stale ring bytes, decoded
     // into the idle W buffer and never read (keeps the MFMA segments straight-line, so the
     // decode VALU interleaves with the MFMAs)
-    sw = read_scale(ps);
-    w0 = read_packed(ps, 0);
+    if constexpr (V != kPlainW) {
+      sw = read_scale(ps);
+      w0 = read_packed(ps, 0);
+    }
     if constexpr (V >= 3) sw.q = sw.q & 0u;
     load_w(b, 0);
     load_x(b, 0);
-    if (dma) dma_w(s + 2, s & 1);
+    if constexpr (V == kPlainW) {
+      if (s + 1 < nsteps) stage_wf(s + 1, b ^ 1);  // retired by this step's phase-3 vmcnt(4)
+    } else if (dma) {
+      dma_w(s + 2, s & 1);
+    }
     __builtin_amdgcn_s_barrier();
     QZ_ST8(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(0, 0);
-    make_table(s + 1, sw, t);
+    if constexpr (V != kPlainW) make_table(s + 1, sw, t);
     decode_dword(w0, b ^ 1, 0, t);
     interleave_mfma_valu<4>();
     __builtin_amdgcn_s_setprio(0);
     QZ_ST8(2);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 1: (rows hi, tokens lo) ----------------
-    w1 = read_packed(ps, 1);
-    w2 = read_packed(ps, 2);
+    if constexpr (V != kPlainW) {
+      w1 = read_packed(ps, 1);
+      w2 = read_packed(ps, 2);
+    }
     load_w(b, 1);
     if (dma) {  // quarters 0 (group 0, tokens lo) and 2 (group 1, tokens lo): last read in phase 0
       stage_xq(s + 2, b, 0);
@@ -764,7 +793,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(4);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 2: (rows hi, tokens hi) ----------------
-    w3 = read_packed(ps, 3);
+    if constexpr (V != kPlainW) w3 = read_packed(ps, 3);
     load_x(b, 1);
     __builtin_amdgcn_s_barrier();
     QZ_ST8(5);
@@ -801,7 +830,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   }
   if (V != 2 && wt == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
 #ifdef QZ_STAMPS8P
-  if (V == 0 && lane == 0 && nsteps > 10 && (blockIdx.x == 0 || blockIdx.x == 100)) {
+  if ((V == 0 || V == kPlainW) && lane == 0 && nsteps > 10 && (blockIdx.x == 0 || blockIdx.x == 100)) {
     for (int k = 0; k < 9; ++k) g_qz_stamp8p[((blockIdx.x ? 1 : 0) * 8 + wave) * 16 + k] = st8[k];
   }
 #endif
@@ -1065,6 +1094,45 @@ static void gemm_plan(int T, int M, int K, long long ws_bytes, int *bt, int *nsp
 using namespace qz;
 
 static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0; }
+
+extern "C" int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy);
+
+// Dense 16-bit GEMM on the staggered 8-phase schedule (k_gemm_4bit_8p<.., kPlainW>): the second
+// half of the large-T prefill route "dequantise once (qz_dequantize_4bit, bit-exact), then GEMM"
+// (modules.py:62-64's own structure, both halves hand-written for gfx950).
+extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dtype, const void *W, const void *bias,
+                             void *Y, int ldy, void *stream) {
+  if (!X || !W || !Y || T < 0 || M < 0 || K < 0) return QZ_ERR_ARG;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_DTYPE;
+  if (T == 0 || M == 0) return QZ_OK;
+  if (!qz_gemm_16bit_ok(T, M, K, X, ldx, W, Y, ldy)) return QZ_ERR_SHAPE;
+  GemmParams p{};
+  p.X = X;
+  p.B = reinterpret_cast<const unsigned char *>(W);
+  p.bias = bias;
+  p.Y = Y;
+  p.T = T;
+  p.M = M;
+  p.K = K;
+  p.ldx = ldx;
+  p.ldy = ldy;
+  p.k_split = K;
+  const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == QZ_DT_F16)
+    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, kPlainW>), dim3(g), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_BF16, kPlainW>), dim3(g), dim3(512), 0, s, p);
+  QZ_LAUNCH_CHECK();
+  return QZ_OK;
+}
+
+extern "C" int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy) {
+  return T > 0 && M > 0 && K > 0 && K % kBK == 0 && M % 8 == 0 && ldx >= K && ldx % 8 == 0 && ldy >= M &&
+         ldy % 8 == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 && (reinterpret_cast<uintptr_t>(W) % 16) == 0 &&
+         (reinterpret_cast<uintptr_t>(Y) % 16) == 0 && (long long)T * ldx * 2 < (1LL << 32) &&
+         (long long)M * K * 2 < (1LL << 32);
+}
 
 extern "C" long long qz_gemm_4bit_workspace_size(int T, int M, int K) {
   if (T <= 0 || M <= 0 || K <= 0 || K % kBK != 0) return 0;

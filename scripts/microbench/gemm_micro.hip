@@ -44,6 +44,9 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&X, (size_t)TMAX * K * 2));
   hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, reinterpret_cast<uint32_t *>(X), (long long)TMAX * K / 2, 9u, 0xBBFFBBFFu, 0u);
   CK(hipMalloc(&Y, (size_t)TMAX * M * 2));
+  void *W16;  // fp16 weights for the plain-GEMM schedule variant (V = 5)
+  CK(hipMalloc(&W16, (size_t)M * K * 2));
+  hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, reinterpret_cast<uint32_t *>(W16), (long long)M * K / 2, 5u, 0xBBFFBBFFu, 0u);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   GemmParams p{};
   p.X = X; p.Y = Y; p.B = B; p.sc = ScaleSrc{nullptr, Q, A2, code2, off, 256};
@@ -61,7 +64,11 @@ int main(int argc, char **argv) {
 #define P8V(V_) vs.push_back({"8phase V=" #V_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
       const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
       hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, V_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { BIGV(3); P8V(0); P8V(1); P8V(2); P8V(3); P8V(4); }
+    if (T >= 4096) { BIGV(3); P8V(0); P8V(1); P8V(3); P8V(4);
+      vs.push_back({"8phase V=5 (plain fp16 GEMM) T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T;
+        q.B = reinterpret_cast<const unsigned char *>(W16);
+        const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256));
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 5>), dim3(g), dim3(512), 0, 0, q); }, {}}); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());

@@ -546,7 +546,7 @@ template <int N> __device__ __forceinline__ void interleave_mfma_valu() {
 constexpr int kPlainW = 5;  // k_gemm_4bit_8p variant: B is a dense 16-bit [M, K] weight (qz_gemm_16bit)
 constexpr int k8pX = 0, k8pW = 2 * kBigStage, k8pWp = 4 * kBigStage, k8pSc = k8pWp + 2 * kBigWp;
 constexpr int k8pCode2 = k8pSc + 2 * 2048;
-template <int QT, bool DQ, int DT, int V = 0>
+template <int QT, bool DQ, int DT, int V = 0, int SK = 0>
 __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[k8pCode2 + (DQ ? 1024 : 0)];
   typedef __attribute__((address_space(3))) void *lds_ptr_t;
@@ -662,7 +662,10 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
   v4u xf[2][4];  // X fragments of the current token half: [kk][i]
-  v4u wf[2][2];  // W fragments of the current row half: [kk][j]
+  // W fragments [kk][j] of row half 0 (wfA) and 1 (wfB); without SK & 1 both names are one set
+  // (reloaded in phase 3), with it rows-lo stay live from phase 0 to phase 3
+  v4u wfA[2][2], wfB0[2][2];
+  v4u(&wfB)[2][2] = (SK & 1) ? wfB0 : wfA;
   auto load_x = [&](int buf, int th) {
     const unsigned char *sx = smem + k8pX + buf * kBigStage + (128 * wt + 64 * th) * 128;
 #pragma unroll
@@ -672,12 +675,14 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   };
   auto load_w = [&](int buf, int rh) {
     const unsigned char *sw = smem + k8pW + buf * kBigStage + (64 * wm + 32 * rh) * 128;
+    v4u(&wf)[2][2] = rh ? wfB : wfA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int j = 0; j < 2; ++j) wf[kk][j] = *reinterpret_cast<const v4u *>(sw + frag_lane[kk] + 16 * j * 128);
   };
   auto mfma_quadrant = [&](int rh, int th) {
+    v4u(&wf)[2][2] = rh ? wfB : wfA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -722,6 +727,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   __syncthreads();
 
   if (V != 2 && wt == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier interval behind
+  if constexpr ((SK & 2) != 0) {  // static priority for the younger half (guide T5, static form)
+    if (wt == 1) __builtin_amdgcn_s_setprio(1);
+  }
 #ifdef QZ_STAMPS8P
   unsigned long long st8[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define QZ_ST8(k)                                                                       \
@@ -762,12 +770,12 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(0, 0);
     if constexpr (V != kPlainW) make_table(s + 1, sw, t);
     decode_dword(w0, b ^ 1, 0, t);
     interleave_mfma_valu<4>();
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(2);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 1: (rows hi, tokens lo) ----------------
@@ -784,12 +792,12 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(3);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(1, 0);
     decode_dword(w1, b ^ 1, 1, t);
     decode_dword(w2, b ^ 1, 2, t);
     interleave_mfma_valu<4>();
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(4);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 2: (rows hi, tokens hi) ----------------
@@ -799,18 +807,18 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(5);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(1, 1);
     decode_dword(w3, b ^ 1, 3, t);
     interleave_mfma_valu<2>();
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     // the W(s+1) image is complete: every wave's stores retired before this barrier (>= 3
     // barriers before step s+1's first read of it)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     QZ_ST8(6);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 3: (rows lo, tokens hi); retire the step's staging ----------------
-    load_w(b, 0);
+    if constexpr ((SK & 1) == 0) load_w(b, 0);
     if (dma) {  // quarters 1 and 3 (tokens hi): last read in phase 2
       stage_xq(s + 2, b, 1);
       stage_xq(s + 2, b, 3);
@@ -822,9 +830,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(7);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(0, 1);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(8);
     __builtin_amdgcn_s_barrier();
   }

@@ -64,11 +64,14 @@ int main(int argc, char **argv) {
 #define P8V(V_) vs.push_back({"8phase V=" #V_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
       const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
       hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, V_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { BIGV(3); P8V(0); P8V(1); P8V(3); P8V(4);
-      vs.push_back({"8phase V=5 (plain fp16 GEMM) T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T;
-        q.B = reinterpret_cast<const unsigned char *>(W16);
-        const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256));
-        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 5>), dim3(g), dim3(512), 0, 0, q); }, {}}); }
+#define PLV(SK_) vs.push_back({"plain fp16 GEMM SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
+        q.B = reinterpret_cast<const unsigned char *>(W16); \
+        const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, 5, SK_>), dim3(g), dim3(512), 0, 0, q); }, {}})
+#define P8S(SK_) vs.push_back({"8phase V=0 SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
+        const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, SK_>), dim3(g), dim3(512), 0, 0, q); }, {}})
+    if (T >= 4096) { P8S(0); P8S(1); P8S(2); P8S(3); PLV(0); PLV(1); PLV(2); PLV(3); PLV(4); PLV(5); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());

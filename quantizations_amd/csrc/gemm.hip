@@ -527,6 +527,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 //     exact fp16/bf16 image) per thread per phase, into the other W buffer; the
 //     per-(row, block) table is built in phase 0.  Phase 3 waits lgkmcnt(0) before
 //     its barrier, so the image is complete before any wave reads it.
+// SK (schedule knobs; the product uses 1): 1 = keep the rows-lo W fragments live from phase 0
+// to phase 3 instead of re-reading them (+2 % fused); 2 = one static s_setprio for group 1
+// instead of per-cluster flips, 4 = no s_setprio (both slower: profiles/r2_gemm_sk.txt).
 // V (microbenchmark A/B, timing only except 0, 2 and 5): 0 = product; 1 = no decode
 // (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
 // 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone); 5 = a plain fp16 GEMM on the
@@ -1128,9 +1131,9 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == QZ_DT_F16)
-    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, kPlainW>), dim3(g), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, kPlainW, 1>), dim3(g), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_BF16, kPlainW>), dim3(g), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_BF16, kPlainW, 1>), dim3(g), dim3(512), 0, s, p);
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }
@@ -1217,7 +1220,7 @@ extern "C" int qz_gemm_4bit(int T, int M, int K, const void *X, int ldx, int dty
     p.ws = nullptr;
     p.k_split = K;
     const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
-#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_8p<QT_, DQ_, DT_, 0>), dim3(g), dim3(512), 0, s, p)
+#define QZ_BIG(QT_, DQ_, DT_) hipLaunchKernelGGL((k_gemm_4bit_8p<QT_, DQ_, DT_, 0, 1>), dim3(g), dim3(512), 0, s, p)
 #define QZ_BIG_DT(QT_, DQ_) \
   do { if (dtype == QZ_DT_F16) QZ_BIG(QT_, DQ_, QZ_DT_F16); else QZ_BIG(QT_, DQ_, QZ_DT_BF16); } while (0)
     if (quant_type == QZ_FP4) {

@@ -529,7 +529,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 //     its barrier, so the image is complete before any wave reads it.
 // SK (schedule knobs; the product uses 1): 1 = keep the rows-lo W fragments live from phase 0
 // to phase 3 instead of re-reading them (+2 % fused); 2 = one static s_setprio for group 1
-// instead of per-cluster flips, 4 = no s_setprio (both slower: profiles/r2_gemm_sk.txt).
+// instead of per-cluster flips, 4 = no s_setprio (both slower: profiles/r2_gemm_sk.txt);
+// 8 = v_mfma_f32_32x32x16 instead of 16x16x32 (same results bit for bit, 7-11 % slower:
+// profiles/r2_gemm_mfma32.txt).
 // V (microbenchmark A/B, timing only except 0, 2 and 5): 0 = product; 1 = no decode
 // (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
 // 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone); 5 = a plain fp16 GEMM on the
@@ -537,11 +539,11 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 #ifdef QZ_STAMPS8P
 __device__ unsigned long long g_qz_stamp8p[2 * 8 * 16];
 #endif
-// scheduling hint for one MFMA segment: 16 x {1 MFMA, N VALU} (the decode's VALU goes into the
+// scheduling hint for one MFMA segment: NM x {1 MFMA, N VALU} (the decode's VALU goes into the
 // issue slots the MFMAs leave free instead of queueing after the last one)
-template <int N> __device__ __forceinline__ void interleave_mfma_valu() {
+template <int N, int NM = 16> __device__ __forceinline__ void interleave_mfma_valu() {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NM; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x002, N, 0);
   }
@@ -669,8 +671,37 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   // (reloaded in phase 3), with it rows-lo stay live from phase 0 to phase 3
   v4u wfA[2][2], wfB0[2][2];
   v4u(&wfB)[2][2] = (SK & 1) ? wfB0 : wfA;
+  // SK & 8: the same quadrants on v_mfma_f32_32x32x16 (8 MFMAs of 32 cycles per phase instead of
+  // 16 of 16: half the MFMA issue slots, so more room for the other group's reads and the decode).
+  // A/B lane (r32 = lane % 32, h32 = lane / 32) holds row r32, k = 8 h32 .. +8 of a k16 substep q
+  // (chunk 2q + h32); the swizzle of lds_off keeps every ds_read_b128 lane group conflict-free.
+  // D: lane holds column (token) r32, rows 8g + 4 h32 + r in register 4g + r.
+  constexpr bool kMF32 = (SK & 8) != 0;
+  typedef float f16v_t __attribute__((ext_vector_type(16)));
+  const int r32 = lane & 31, h32 = lane >> 5;
+  uint32_t fl32[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) fl32[q] = (uint32_t)(r32 * 128 + (((2 * q + h32) ^ ((r32 >> 1) & 7)) << 4));
+  f16v_t acc32[kMF32 ? 2 : 1][kMF32 ? 4 : 1];
+  if constexpr (kMF32) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[j][i][e] = 0.0f;
+  }
+  v4u xf32[4][2], wfA32[4], wfB32_0[4];
+  v4u(&wfB32)[4] = (SK & 1) ? wfB32_0 : wfA32;
   auto load_x = [&](int buf, int th) {
     const unsigned char *sx = smem + k8pX + buf * kBigStage + (128 * wt + 64 * th) * 128;
+    if constexpr (kMF32) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) xf32[q][i] = *reinterpret_cast<const v4u *>(sx + 32 * i * 128 + fl32[q]);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -678,6 +709,12 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   };
   auto load_w = [&](int buf, int rh) {
     const unsigned char *sw = smem + k8pW + buf * kBigStage + (64 * wm + 32 * rh) * 128;
+    if constexpr (kMF32) {
+      v4u(&wf32)[4] = rh ? wfB32 : wfA32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wf32[q] = *reinterpret_cast<const v4u *>(sw + fl32[q]);
+      return;
+    }
     v4u(&wf)[2][2] = rh ? wfB : wfA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -685,6 +722,22 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
       for (int j = 0; j < 2; ++j) wf[kk][j] = *reinterpret_cast<const v4u *>(sw + frag_lane[kk] + 16 * j * 128);
   };
   auto mfma_quadrant = [&](int rh, int th) {
+    if constexpr (kMF32) {
+      v4u(&wf32)[4] = rh ? wfB32 : wfA32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          f16v_t &c = acc32[rh][2 * th + i];
+          if constexpr (DT == QZ_DT_F16)
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, wf32[q]),
+                                                       __builtin_bit_cast(h8_t, xf32[q][i]), c, 0, 0, 0);
+          else
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8_t, wf32[q]),
+                                                        __builtin_bit_cast(b8_t, xf32[q][i]), c, 0, 0, 0);
+        }
+      return;
+    }
     v4u(&wf)[2][2] = rh ? wfB : wfA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -777,7 +830,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     mfma_quadrant(0, 0);
     if constexpr (V != kPlainW) make_table(s + 1, sw, t);
     decode_dword(w0, b ^ 1, 0, t);
-    interleave_mfma_valu<4>();
+    if constexpr (kMF32) interleave_mfma_valu<8, 8>(); else interleave_mfma_valu<4>();
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(2);
     __builtin_amdgcn_s_barrier();
@@ -799,7 +852,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     mfma_quadrant(1, 0);
     decode_dword(w1, b ^ 1, 1, t);
     decode_dword(w2, b ^ 1, 2, t);
-    interleave_mfma_valu<4>();
+    if constexpr (kMF32) interleave_mfma_valu<8, 8>(); else interleave_mfma_valu<4>();
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(4);
     __builtin_amdgcn_s_barrier();
@@ -813,7 +866,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(1, 1);
     decode_dword(w3, b ^ 1, 3, t);
-    interleave_mfma_valu<2>();
+    if constexpr (kMF32) interleave_mfma_valu<4, 8>(); else interleave_mfma_valu<2>();
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     // the W(s+1) image is complete: every wave's stores retired before this barrier (>= 3
     // barriers before step s+1's first read of it)
@@ -850,24 +903,50 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   __syncthreads();
   unsigned char *ew = smem + wave * (64 * kBigERow);
   float bv[4][4];
+  if constexpr (!kMF32) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = min(m0 + 64 * wm + 16 * j + 4 * fk + r, p.M - 1);
-      bv[j][r] = p.bias ? load_f32<DT>(p.bias, m) : 0.0f;
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int m = min(m0 + 64 * wm + 16 * j + 4 * fk + r, p.M - 1);
+        bv[j][r] = p.bias ? load_f32<DT>(p.bias, m) : 0.0f;
+      }
+  } else {  // bv[jm * 2 + ... ]: rows 32 jm + 8 g + 4 h32 + r -> bv[2 jm + g / 2][...]: indexed below
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = 0.0f;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    if constexpr (kMF32) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int jm = 0; jm < 2; ++jm)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f4_t v = acc[j][4 * h + i];
-        const uint32_t lo = cvt_pk16<DT>(v[0] + bv[j][0], v[1] + bv[j][1]);
-        const uint32_t hi = cvt_pk16<DT>(v[2] + bv[j][2], v[3] + bv[j][3]);
-        *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * kBigERow + (16 * j + 4 * fk) * 2) = uint2{lo, hi};
-      }
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f16v_t &v = acc32[jm][2 * h + i];
+            const int row = 32 * jm + 8 * g + 4 * h32;
+            float b4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              b4[r] = p.bias ? load_f32<DT>(p.bias, min(m0 + 64 * wm + row + r, p.M - 1)) : 0.0f;
+            const uint32_t lo = cvt_pk16<DT>(v[4 * g] + b4[0], v[4 * g + 1] + b4[1]);
+            const uint32_t hi = cvt_pk16<DT>(v[4 * g + 2] + b4[2], v[4 * g + 3] + b4[3]);
+            *reinterpret_cast<uint2 *>(ew + (32 * i + r32) * kBigERow + row * 2) = uint2{lo, hi};
+          }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f4_t v = acc[j][4 * h + i];
+          const uint32_t lo = cvt_pk16<DT>(v[0] + bv[j][0], v[1] + bv[j][1]);
+          const uint32_t hi = cvt_pk16<DT>(v[2] + bv[j][2], v[3] + bv[j][3]);
+          *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * kBigERow + (16 * j + 4 * fk) * 2) = uint2{lo, hi};
+        }
+    }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int qd = lane + 64 * it, tok = qd >> 3, c16 = qd & 7;

@@ -71,7 +71,7 @@ int main(int argc, char **argv) {
 #define P8S(SK_) vs.push_back({"8phase V=0 SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
         const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
         hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, SK_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { P8S(0); P8S(1); P8S(2); P8S(3); PLV(0); PLV(1); PLV(2); PLV(3); PLV(4); PLV(5); }
+    if (T >= 4096) { P8S(1); P8S(9); P8S(8); PLV(1); PLV(9); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());
@@ -87,6 +87,34 @@ int main(int argc, char **argv) {
       v.us.push_back(ms * 1e3 / it);
     }
   printf("M=%d K=%d NF4+DQ f16, random operands\n", M, K);
+  {  // 32x32x16 (SK 9) vs 16x16x32 (SK 1) results: same operands, fp32 sums in another order
+    void *Y2; CK(hipMalloc(&Y2, (size_t)4096 * M * 2));
+    GemmParams q = p; q.T = 4096;
+    const unsigned g = (unsigned)(((M + 255) / 256) * ((4096 + 255) / 256));
+    for (int plain = 0; plain < 2; ++plain) {
+      GemmParams a = q, b2 = q; b2.Y = Y2;
+      if (plain) { a.B = b2.B = reinterpret_cast<const unsigned char *>(W16); }
+      if (plain) {
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, 5, 1>), dim3(g), dim3(512), 0, 0, a);
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, 5, 9>), dim3(g), dim3(512), 0, 0, b2);
+      } else {
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, 1>), dim3(g), dim3(512), 0, 0, a);
+        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, 9>), dim3(g), dim3(512), 0, 0, b2);
+      }
+      CK(hipDeviceSynchronize());
+      std::vector<uint16_t> h1((size_t)4096 * M), h2((size_t)4096 * M);
+      CK(hipMemcpy(h1.data(), Y, h1.size() * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), Y2, h2.size() * 2, hipMemcpyDeviceToHost));
+      double maxd = 0, maxv = 0; size_t ndiff = 0;
+      for (size_t i = 0; i < h1.size(); ++i) {
+        const float a1 = (float)__builtin_bit_cast(_Float16, h1[i]), a2 = (float)__builtin_bit_cast(_Float16, h2[i]);
+        maxd = std::max(maxd, (double)std::fabs(a1 - a2)); maxv = std::max(maxv, (double)std::fabs(a1));
+        ndiff += h1[i] != h2[i];
+      }
+      printf("check %s: SK9 vs SK1 max|diff| %.4g (max|y| %.4g), %zu of %zu elements differ\n", plain ? "plain" : "fused",
+             maxd, maxv, ndiff, h1.size());
+    }
+  }
 #ifdef STAMPS
   {
     unsigned long long h[2 * 8 * 16];

@@ -4,7 +4,9 @@ The 4-bit layer is independent per output row, so rank p of P keeps rows
 [p*M/P, (p+1)*M/P).  In the flat row-major layout that is a contiguous slice
 of the packed bytes, of the per-block scales and (with double quant) of the
 256-block second-level scales -- the GLOBAL quant state is sliced, never
-re-quantised, so every rank's rows are bit-identical to the single-GPU layer.
+re-quantised, so every rank multiplies exactly the single-GPU layer's weights
+(outputs equal up to fp32 summation order where the shard's launch geometry
+differs).
 x is replicated; after the local fused GEMV/GEMM the fp16 row shards are
 exchanged with ``all_gather_into_tensor`` (RCCL over xGMI on MI355X, gloo in
 the CPU tests).  The reference has no multi-GPU path; this is the build's

@@ -897,3 +897,38 @@ def test_tensor_parallel_pair_world1_rccl():
         assert torch.isfinite(step).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("M,K", [(8192, 8192), (1024, 8192), (28672, 8192), (8192, 28672)])
+def test_config5_70b_rowsplit_shards_on_one_gpu(M, K):
+    """Config #5's layout at its workload, rank by rank on one GPU: every
+    Llama-3-70B Linear4bit shape row-split 8 ways exactly as parallel.shard_rows
+    gives each rank (slices of the global quant state + block_base).  The
+    all-gather order (rank-major concatenation) of the ranks' fused GEMVs matches
+    an fp64 product of the bit-exact dequantised weight, as the unsharded launch
+    does; a shard differs from the unsharded rows only by fp32 summation order
+    (a smaller grid splits K over more waves), i.e. at most one fp16 ulp."""
+    from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
+    from quantizations_amd.parallel import shard_rows
+
+    torch.manual_seed(M ^ K)
+    W = (torch.randn(M, K, device=DEV) * 0.02).half()
+    packed, st = quantize_4bit(W, quant_type="nf4")
+    del W
+    x = torch.randn(1, 1, K, device=DEV).half()
+    full = gemv_4bit(x, packed, state=st)
+    world = 8
+    parts = []
+    for r in range(world):
+        sh = shard_rows(packed, st, r, world)
+        y = gemv_4bit(x, sh.packed, state=sh.state, block_base=sh.block_base)
+        parts.append(y.reshape(-1))
+    gathered = torch.cat(parts)
+    d = (gathered.float() - full.reshape(-1).float()).abs()
+    ulp = torch.finfo(torch.float16).eps * full.reshape(-1).float().abs().clamp_min(2.0 ** -14)
+    assert bool((d <= ulp).all()), float((d / ulp).max())
+    wd = dequantize_4bit(packed, st, out_dtype=torch.float32).t()
+    ref = (wd.double() @ x.double().reshape(K, 1)).reshape(1, M)
+    del wd
+    assert_close(full.float().cpu().reshape(1, M), ref.cpu().numpy(), torch.float16, f"70B {M}x{K}")
+    assert_close(gathered.float().cpu().reshape(1, M), ref.cpu().numpy(), torch.float16, f"70B 8-way {M}x{K}")

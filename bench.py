@@ -732,8 +732,9 @@ def main():
                        f"{args.quant.upper()} bs=1; 4096×4096 GEMV GB/s vs HBM peak"),
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f16 activations x 4-bit NF4 weights, fp32 accumulate",
-            "data": "synthetic (random-init Llama-3-8B architecture, random prompt)",
+            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": f"f16 activations x 4-bit {args.quant.upper()} weights, fp32 accumulate",
+            "data": f"synthetic (random-init {'Llama-3-70B' if args.model == 'llama3-70b' else 'Llama-3-8B'} "
+                    "architecture, random prompt)",
             "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}-decode-bs1",
                        "layers": cfg.num_hidden_layers,
                        "prompt_len": args.prompt, "global_batch": gbatch, "streams_per_gpu": gbatch / world,

@@ -531,7 +531,10 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 // to phase 3 instead of re-reading them (+2 % fused); 2 = one static s_setprio for group 1
 // instead of per-cluster flips, 4 = no s_setprio (both slower: profiles/r2_gemm_sk.txt);
 // 8 = v_mfma_f32_32x32x16 instead of 16x16x32 (same results bit for bit, 7-11 % slower:
-// profiles/r2_gemm_mfma32.txt).
+// profiles/r2_gemm_mfma32.txt); 16 = no DMA at all and 32 = every step DMAs the k-slice of step 0
+// (microbenchmark timing only: the LDS -> MFMA skeleton, and the schedule with L2-resident
+// operands); 64 = grouped (4 token x 8 row tiles per XCD) tile order; 128 = plain W staged
+// through registers.
 // V (microbenchmark A/B, timing only except 0, 2 and 5): 0 = product; 1 = no decode
 // (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
 // 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone); 5 = a plain fp16 GEMM on the
@@ -566,8 +569,20 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int m0 = (wg % tiles_m) * kBigM, t0 = (wg / tiles_m) * kBigT;
+  int tm = wg % tiles_m, tt = wg / tiles_m;
+  if constexpr ((SK & 64) != 0) {
+    // grouped order: the tiles of one XCD in flight together cover 4 token tiles x 8 row tiles
+    // (X and W k-slices each shared by 8 resp. 4 of them in that XCD's L2) instead of 2 x 16
+    const int tiles_t = (p.T + kBigT - 1) / kBigT;
+    if (tiles_m % 8 == 0 && tiles_t % 4 == 0) {
+      const int grp = wg / (4 * tiles_m), r = wg % (4 * tiles_m);
+      tt = 4 * grp + (r % 32) / 8;
+      tm = 8 * (r / 32) + r % 8;
+    }
+  }
+  const int m0 = tm * kBigM, t0 = tt * kBigT;
   const int nsteps = p.K / kBK;
+  constexpr uint32_t kStepB = (SK & 32) ? 0u : (uint32_t)(kBK * 2);  // SK & 32: timing only
 
   // ---- staging (LDS DMA only) ----
   const unsigned char *xbase = reinterpret_cast<const unsigned char *>(p.X);
@@ -580,8 +595,8 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   }
   // instruction i of every wave stages token quarter i (rows 64 i .. 64 i + 63 of the tile)
   auto stage_xq = [&](int step, int buf, int i) {
-    if constexpr (V == 4) return;
-    __builtin_amdgcn_global_load_lds((glb_ptr_t)(xbase + xoff[i] + (uint32_t)step * (kBK * 2)),
+    if constexpr (V == 4 || (SK & 16) != 0) return;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(xbase + xoff[i] + (uint32_t)step * kStepB),
                                      (lds_ptr_t)(smem + k8pX + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
   };
   // V == kPlainW (qz_gemm_16bit): B is a dense 16-bit [M, K] weight staged by DMA like X, one
@@ -593,10 +608,24 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     const int chunk = (lane & 7) ^ ((row >> 1) & 7);
     woff[i] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * chunk) * 2u;
   }
-  auto stage_wf = [&](int step, int buf) {
+  // SK & 128: W through registers instead (global_load_dwordx4 in phase 0, ds_write_b128 in
+  // phase 2's MFMA segment) -- no LDS-DMA issue for W
+  v4u wreg[4];
+  auto load_wf_regs = [&](int step) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + woff[i] + (uint32_t)step * (kBK * 2)),
+      wreg[i] = *reinterpret_cast<const v4u *>(p.B + woff[i] + (uint32_t)step * kStepB);
+  };
+  auto write_wf_regs = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<v4u *>(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024 + lane * 16) = wreg[i];
+  };
+  auto stage_wf = [&](int step, int buf) {
+    if constexpr ((SK & 16) != 0) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + woff[i] + (uint32_t)step * kStepB),
                                        (lds_ptr_t)(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
   };
   const int wr = tid >> 1, wh = tid & 1;  // decode ownership: row wr, 32-code half wh
@@ -817,7 +846,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     if constexpr (V >= 3) sw.q = sw.q & 0u;
     load_w(b, 0);
     load_x(b, 0);
-    if constexpr (V == kPlainW) {
+    if constexpr (V == kPlainW && (SK & 128) != 0) {
+      load_wf_regs(min(s + 1, nsteps - 1));         // written in phase 2 (stale in the last step)
+    } else if constexpr (V == kPlainW) {
       if (s + 1 < nsteps) stage_wf(s + 1, b ^ 1);  // retired by this step's phase-3 vmcnt(4)
     } else if (dma) {
       dma_w(s + 2, s & 1);
@@ -865,6 +896,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     __builtin_amdgcn_sched_barrier(0);
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(1);
     mfma_quadrant(1, 1);
+    if constexpr (V == kPlainW && (SK & 128) != 0) write_wf_regs(b ^ 1);
     decode_dword(w3, b ^ 1, 3, t);
     if constexpr (kMF32) interleave_mfma_valu<4, 8>(); else interleave_mfma_valu<2>();
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);

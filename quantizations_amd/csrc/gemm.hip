@@ -990,6 +990,199 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_gemm16_4w: 256 x 256 tile, 4 waves (one per SIMD), each wave a 128-token x 128-row quadrant.
+//
+// Why not the 8-wave schedule for a dense 16-bit B: with 8 waves a step re-reads the staged tile
+// 3x from LDS (each wave its 128 x 64 X and 64 x 64 W slices: 192 KB per 256 x 256 x 64 step);
+// four 128 x 128 quadrants read 128 KB, the ratio hipBLASLt's MT256x256x64 tile runs at.  The
+// 8-wave skeleton with no staging at all peaks at 1.58 PFLOP/s (gemm_micro SK 17,
+// profiles/r2_gemm_nodma.txt) and its LDS-DMA staging costs a further 20 %.
+//
+// Registers per lane: 64 accumulators (8 x 8 16x16 tiles, the 256 AGPRs); the X fragments of
+// the current and the next k-half (2 x 32); a 4-slot ring of W fragments streamed two MFMA rows
+// ahead (16); the step-after-next's global bytes (16 x 16 B staging, global_load_dwordx4: no
+// LDS-DMA issue cost).  A k-half is 8 rows j of 8 MFMAs (acc[j][*] += W_j . X_*), each row
+// pinned by sched_barrier together with its share of the memory work:
+//   half (s, 0): row j also writes staging chunk j (step s+1) into buffer (s+1)&1, refills it
+//                with step s+2 (a whole step of latency cover), reads X fragment j of k-half 1
+//                and W fragment j+2 (k-half 1 past 7); lgkmcnt(0); s_barrier
+//   half (s, 1): row j reads X fragment j of step s+1's k-half 0 (buffer (s+1)&1) and the next W
+//                fragment; s_barrier
+// Buffer (s+1)&1 is rewritten in half (s, 0): its last reads were in half (s-1, 1) (behind the
+// barrier ending it); buffer s&1 is rewritten in half (s+1, 0), behind the barrier ending (s, 1).
+// The last steps load/write clamped (stale) data instead of branching.
+constexpr int k4wT = 256, k4wM = 256;
+constexpr int k4wStage = 256 * 128;                 // one buffer of X or W: 256 rows x 64 x 2 B
+constexpr int k4wERow = 272;                        // epilogue image row: 128 outputs x 2 B + 16 B
+constexpr int k4wLds = (4 * k4wStage > 4 * 128 * k4wERow) ? 4 * k4wStage : 4 * 128 * k4wERow;
+template <int DT, int SK = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4w(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[k4wLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 1, wm = wave & 1;
+
+  // XCD-aware, bijective tile order (as k_gemm_4bit_big)
+  const int tiles_m = (p.M + k4wM - 1) / k4wM;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int m0 = (wg % tiles_m) * k4wM, t0 = (wg / tiles_m) * k4wT;
+  const int nsteps = p.K / kBK;
+
+  // staging: thread t moves 16-B chunk (t & 7) of rows 32 c + t / 8, c = 0..7, of X and of W
+  const unsigned char *xg = reinterpret_cast<const unsigned char *>(p.X);
+  uint32_t xo[8], wo[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int row = 32 * c + (tid >> 3), ch = tid & 7;
+    xo[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * ch) * 2u;
+    wo[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * ch) * 2u;
+  }
+  const uint32_t lo = (uint32_t)lds_off(tid >> 3, tid & 7);  // + 4 KiB per c: same swizzle
+  v4u xs[8], ws[8];
+  // SK (timing only, gemm_micro): 1 = no staging in the loop, 2 = no fragment reads in the loop,
+  // 4 = every step stages step 0 (L2-resident operands); 8 = LDS-DMA staging (rows 0..3 of half 0);
+  // 16 = global loads only, 32 = LDS stores only
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  typedef __attribute__((address_space(1))) void *glb_ptr_t;
+  const uint32_t dsw = 16u * (uint32_t)((tid & 7) ^ ((tid >> 4) & 7)) - 16u * (uint32_t)(tid & 7);
+  auto dma = [&](int step, int buf, int c) {
+    const uint32_t kb = (SK & 4) ? 0u : (uint32_t)step * (kBK * 2);
+    unsigned char *bx = smem + buf * (2 * k4wStage) + 4096 * c + wave * 1024;
+    // (dsw wraps: add the 32-bit offsets first, then to the pointer)
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(xg + (uint32_t)(xo[c] + dsw + kb)), (lds_ptr_t)bx, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + (uint32_t)(wo[c] + dsw + kb)), (lds_ptr_t)(bx + k4wStage), 16,
+                                     0, 0);
+  };
+  auto gload = [&](int step, int c) {
+    const uint32_t kb = (SK & 4) ? 0u : (uint32_t)step * (kBK * 2);
+    xs[c] = *reinterpret_cast<const v4u *>(xg + xo[c] + kb);
+    ws[c] = *reinterpret_cast<const v4u *>(p.B + wo[c] + kb);
+  };
+  auto swrite = [&](int buf, int c) {
+    unsigned char *bx = smem + buf * (2 * k4wStage);
+    *reinterpret_cast<v4u *>(bx + lo + 4096 * c) = xs[c];
+    *reinterpret_cast<v4u *>(bx + k4wStage + lo + 4096 * c) = ws[c];
+  };
+
+  // fragments: lane (fr, fk) of a 16 x 32 operand holds row fr, k 8 fk .. +8 of the k-half
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                          (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  v4u xf[2][8], wr[4];
+  auto xread = [&](int buf, int kk, int i) {
+    xf[kk][i] = *reinterpret_cast<const v4u *>(smem + buf * (2 * k4wStage) + (128 * wt + 16 * i) * 128 + fl[kk]);
+  };
+  auto wread = [&](int buf, int kk, int j) {  // W fragment j of k-half kk into ring slot (8 kk + j) & 3
+    wr[j & 3] = *reinterpret_cast<const v4u *>(smem + buf * (2 * k4wStage) + k4wStage + (128 * wm + 16 * j) * 128 +
+                                               fl[kk]);
+  };
+  f4_t acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+  auto mfma_row = [&](int kk, int j) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (DT == QZ_DT_F16)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, wr[j & 3]),
+                                                           __builtin_bit_cast(h8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+      else
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, wr[j & 3]),
+                                                            __builtin_bit_cast(b8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+    }
+  };
+
+  // ---- prologue: step 0 in buffer 0, step 1 in the staging registers, k-half 0's X + W 0, 1 read ----
+#pragma unroll
+  for (int c = 0; c < 8; ++c) gload(0, c);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) swrite(0, c);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) gload(min(1, nsteps - 1), c);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xread(0, 0, i);
+  wread(0, 0, 0);
+  wread(0, 0, 1);
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int b = s & 1;
+    const int s2 = min(s + 2, nsteps - 1);
+    // ---- half (s, 0) ----
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((SK & 8) != 0) {
+        if (j < 4) {
+          dma(min(s + 1, nsteps - 1), b ^ 1, 2 * j);
+          dma(min(s + 1, nsteps - 1), b ^ 1, 2 * j + 1);
+        }
+      } else if constexpr ((SK & 16) != 0) {  // loads only: the registers consumed by an empty asm
+        asm volatile("" ::"v"(xs[j]), "v"(ws[j]));
+        gload(s2, j);
+      } else if constexpr ((SK & 32) != 0) {  // LDS stores only (stale registers)
+        swrite(b ^ 1, j);
+      } else if constexpr ((SK & 1) == 0) {
+        swrite(b ^ 1, j);
+        gload(s2, j);
+      }
+      if constexpr ((SK & 2) == 0) {
+        xread(b, 1, j);
+        if (j < 6) wread(b, 0, j + 2); else wread(b, 1, j - 6);
+      }
+      mfma_row(0, j);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((SK & 8) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- half (s, 1) ----
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((SK & 2) == 0) {
+        xread(b ^ 1, 0, j);
+        if (j < 6) wread(b, 1, j + 2); else wread(b ^ 1, 0, j - 6);
+      }
+      mfma_row(1, j);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // ---- epilogue: quadrant -> LDS image [128 tokens][128 rows] (+ bias) -> coalesced rows ----
+  __syncthreads();
+  unsigned char *ew = smem + wave * (128 * k4wERow);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bv[r] = p.bias ? load_f32<DT>(p.bias, min(m0 + 128 * wm + 16 * j + 4 * fk + r, p.M - 1)) : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f4_t v = acc[j][i];
+      const uint32_t l2 = cvt_pk16<DT>(v[0] + bv[0], v[1] + bv[1]);
+      const uint32_t h2 = cvt_pk16<DT>(v[2] + bv[2], v[3] + bv[3]);
+      *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * k4wERow + (16 * j + 4 * fk) * 2) = uint2{l2, h2};
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int qd = lane + 64 * it, tok = qd >> 4, c16 = qd & 15;
+    const v4u v = *reinterpret_cast<const v4u *>(ew + tok * k4wERow + c16 * 16);
+    const int t = t0 + 128 * wt + tok, m = m0 + 128 * wm + 8 * c16;
+    if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
+  }
+}
+
 // Multi-token GEMV for 2 <= T <= 16 (small-batch decode, short prefills).
 // A 512-thread workgroup owns 16 weight rows; its 8 waves split K and meet in
 // LDS (no workspace, no second launch).  Per 256-element chunk, lane

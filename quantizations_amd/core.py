@@ -514,6 +514,8 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
     if A2.stride(-1) != 1 or A2.data_ptr() % 16 != 0:
         A2 = A2.contiguous()
     T = A2.shape[0]
+    if T == 0 or M == 0:  # an empty batch (F.linear's result; the C-ABI rejects null buffers)
+        return torch.empty((*lead, M), dtype=A.dtype, device=A.device)
     fused_ok = _gemm_fused_ok(A2, state, M, K)
     if route == "fused" and not fused_ok:
         raise ValueError("gemm_4bit: the fused kernel needs fp16/bf16 activations, K % 64 == 0, M % 4 == 0 "

@@ -591,7 +591,9 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
     const uint32_t boff = ((uint32_t)s << 10) + ((uint32_t)lane << 4);
     on = true;
     xb = 2 * (int)boff;
-    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2u * boff);
+    // ABL & 2048 (microbenchmark only): every wave reads its own one of 64 copies of x
+    const void *xp = (ABL & 2048) ? (const void *)((const char *)p.x + (size_t)((row0 / R) & 63) * p.K * 2) : p.x;
+    if constexpr (!XL && !(ABL & 2)) xs.load(xp, 2u * boff);
     const uint32_t lb = (2u * boff) >> p.bs_log2;                 // lane's block within the row
     const uint32_t sb = ((uint32_t)s << 11) >> p.bs_log2;         // step's first block within the row
     const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;              // blocks per row

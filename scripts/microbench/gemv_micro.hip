@@ -186,7 +186,9 @@ int main(int argc, char **argv) {
   }
   float *code2, *off; void *x, *y; uint32_t *sink;
   CK(hipMalloc(&code2, 1024)); CK(hipMemset(code2, 0x3C, 1024)); CK(hipMalloc(&off, 4)); CK(hipMemset(off, 0, 4));
-  CK(hipMalloc(&x, K * 4)); CK(hipMemset(x, 0x3C, K * 4)); CK(hipMalloc(&y, M * 4)); CK(hipMalloc(&sink, 4));
+  // x: 64 copies (ABL & 2048 gives every wave its own)
+  CK(hipMalloc(&x, (size_t)K * 4 * 64)); CK(hipMemset(x, 0x3C, (size_t)K * 4 * 64));
+  CK(hipMalloc(&y, M * 4)); CK(hipMalloc(&sink, 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
 
   // Variants are registered, then timed in interleaved rounds (rule 24 of the
@@ -319,6 +321,10 @@ int main(int argc, char **argv) {
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
     const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
     hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, ABL, true>), dim3(g), dim3(256), 0, 0, q); })
+  const bool xcopy = argc > 4 && std::string(argv[4]) == "xcopy";
+  if (xcopy) {  // x hot-spot test: every wave reads its own copy of x (ABL 2048)
+    GVFS(2, 0); GVFS(2, 2048); GVFS(4, 0); GVFS(4, 2048); GVFS(1, 0); GVFS(1, 2048);
+  }
   if (tabab2) {  // full-step table kernel ablations: 1 no scale loads, 2 no x loads, 4 no reduce/store,
                  // 8 no DPP reduction, 16 no dots, 32 no LDS reads, 64 no table build, 128 no prologue barrier
     GVFS(2, 0); GVFS(2, 1); GVFS(2, 2); GVFS(2, 3); GVFS(2, 4); GVFS(2, 16); GVFS(2, 32); GVFS(2, 48);
@@ -343,7 +349,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

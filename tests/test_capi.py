@@ -74,3 +74,19 @@ def test_argument_errors_are_reported_not_launched():
     assert L.qz_silu_mul(1, 1, 9, 16, 1, 0) == -4
     assert L.qz_add_rmsnorm(1, 0, 0, 4, 64, 64, 1, 1e-6, 1, 1, 64, 0) == -1  # residual required
     assert L.qz_add_rmsnorm(1, 1, 0, 4, 64, 64, 1, 1e-6, 0, 1, 64, 0) == -1  # sum output required
+
+
+def test_gemm16_and_gemm4_guards_without_gpu():
+    # qz_gemm_16bit_ok is a pure host check; shape/dtype/null errors return before any launch
+    from quantizations_amd import _lib
+
+    L = _lib.lib
+    assert L.qz_gemm_16bit_ok(256, 256, 4096, 16, 4096, 16, 16, 256) == 1
+    assert L.qz_gemm_16bit_ok(256, 256, 4100, 16, 4100, 16, 16, 256) == 0   # K % 64
+    assert L.qz_gemm_16bit_ok(256, 260, 4096, 16, 4096, 16, 16, 260) == 0   # M % 8
+    assert L.qz_gemm_16bit_ok(256, 256, 4096, 8, 4096, 16, 16, 256) == 0    # X not 16-B aligned
+    assert L.qz_gemm_16bit_ok(256, 256, 4096, 16, 4000, 16, 16, 256) == 0   # ldx < K
+    assert L.qz_gemm_16bit(1, 8, 100, 16, 100, 1, 16, 0, 16, 8, 0) == -3    # K % 64: shape error
+    assert L.qz_gemm_16bit(1, 8, 64, 16, 64, 7, 16, 0, 16, 8, 0) == -4      # dtype
+    assert L.qz_gemm_16bit(1, 8, 64, 0, 64, 1, 16, 0, 16, 8, 0) == -1       # null X
+    assert L.qz_gemm_16bit(0, 8, 64, 16, 64, 1, 16, 0, 16, 8, 0) == 0       # empty: nothing to do

@@ -308,6 +308,8 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
 
     blocked(empty)
     empty_us = e0.elapsed_time(e1) * 1e3 / iters
+    q = statistics.quantiles(us, n=10)
+    GEMV_EXTRA["per_launch_event_us_p10"], GEMV_EXTRA["per_launch_event_us_p90"] = round(q[0], 3), round(q[-1], 3)
     GEMV_EXTRA["codes"] = "exact (fp32 as hi+lo fp16)" if prod_qt & _lib.EXACT_CODES else "fp16"
     GEMV_EXTRA["other_codes_launch_us"] = round(alt_us, 3)
     return statistics.mean(us), statistics.median(us), b2b_us, floor_us, empty_us
@@ -406,6 +408,69 @@ def dominant_roofline(copies: int = 8, iters: int = 100):
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+@torch.inference_mode()
+def rowsplit_layer(rank: int, world: int, sharded: bool, M: int = 8192, K: int = 28672, calls: int = 20,
+                   reps: int = 5):
+    """one Llama-3-70B-shaped Linear4bit (M x K NF4+DQ, bs = 1) row-split over
+    the job's ranks -- each rank's GEMV on M/P rows (slices of the ONE global quant state)
+    + the RCCL all-gather of the fp16 shards -- vs the same layer's unsharded GEMV on one
+    GPU.  `calls` forward calls are captured into one HIP graph and replayed `reps` times;
+    per-call microseconds = the slowest rank's replay time / calls (barrier + sync around)."""
+    import quantizations_amd as qa
+    from quantizations_amd.parallel import RowShardedLinear4bit
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cuda").manual_seed(88)
+    W = (torch.randn(M, K, device=dev, generator=g) * 0.02).half()
+    full = qa.Linear4bit(K, M, bias=False, quant_type="nf4", compress_statistics=True)
+    full.weight = qa.Params4bit(W, requires_grad=False, quant_type="nf4", module=full, compress_statistics=True)
+    del W
+    full = full.to(dev)
+    x = torch.randn(1, 1, K, device=dev, generator=g).half()
+
+    def timed(fn):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(s)
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg, capture_error_mode=CAPTURE_MODE):
+            for _ in range(calls):
+                fn()
+        cg.replay()
+        best = None
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            cg.replay()
+            torch.cuda.synchronize()
+            dt = torch.tensor([time.perf_counter() - t0], device=dev)
+            if world > 1:
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            best = dt.item() if best is None else min(best, dt.item())
+        return round(best / calls * 1e6, 2)
+
+    out = {"layer": f"{M}x{K} NF4+DQ (Llama-3-70B down_proj shape), bs=1", "ranks": world,
+           "unsharded_us": timed(lambda: full(x))}
+    if sharded:
+        try:
+            shard = RowShardedLinear4bit(full, rank, world)
+            out["rows_per_rank"] = shard.r1 - shard.r0
+            out["local_gemv_us"] = timed(lambda: shard.local_forward(x))
+            out["rowsplit_allgather_us"] = timed(lambda: shard(x))
+            ref, got = full(x).reshape(-1), shard(x).reshape(-1)
+            # same products; a shard's GEMV may split K differently (fp32 summation order)
+            out["bit_identical_to_unsharded"] = bool(torch.equal(got, ref))
+            out["max_abs_diff_vs_unsharded"] = float((got.float() - ref.float()).abs().max())
+        except Exception as e:  # reported, never fatal to the headline line
+            out["error"] = f"{type(e).__name__}: {e}"
+    return out
 
 
 @torch.inference_mode()
@@ -704,6 +769,8 @@ def main():
                           "%s codes)" % (int(GEMV_EXTRA.get("codes", "").startswith("exact")), GEMV_EXTRA.get("codes")),
                 "launch_us_avg": round(b2b_us, 3),
                 "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
+                "per_launch_event_us_p10": GEMV_EXTRA.get("per_launch_event_us_p10"),
+                "per_launch_event_us_p90": GEMV_EXTRA.get("per_launch_event_us_p90"),
                 "one_shot_read_floor_us": round(floor_us, 3),
                 "frac_of_one_shot_floor": round(floor_us / b2b_us, 4),
                 # what one launch can reach at all: an empty dependent launch's period
@@ -714,6 +781,10 @@ def main():
                 "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline()}
         parity = gemv_parity()
+
+    layer = None
+    if not args.no_roofline:
+        layer = rowsplit_layer(rank, world, sharded)   # every rank takes part (the all-gather)
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:
@@ -743,6 +814,8 @@ def main():
                        "projection_groups": n_groups, "layer_ops": n_layer_ops},
             "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
+        if layer is not None:
+            line["rowsplit_layer"] = layer
         if extra_weak is not None:
             line["weak_scaling_extra"] = extra_weak
         print(json.dumps(line), flush=True)

@@ -514,12 +514,13 @@ def prefill_bench(T: int = 16384, iters: int = 10):
             res[name] = {"ms": round(ms, 3), "TFLOP/s": round(2.0 * T * M * K / (ms * 1e-3) / 1e12, 1)}
         out[f"{M}x{K}"] = res
         del W, packed, qs
-    from quantizations_amd.core import GEMM16_MIN_TILES, PREFILL_FUSED_MAX_TOKENS, PREFILL_GEMM16
+    from quantizations_amd.core import GEMM16_MIN_TILES, PREFILL_GEMM16, fused_max_tokens
     return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0,
-            "product_route": "fused" if T <= PREFILL_FUSED_MAX_TOKENS else
+            "product_route": "fused" if T <= fused_max_tokens(4096) else
                              ("dequant+gemm16_8phase" if PREFILL_GEMM16 else "dequant+hipblaslt"),
             "note": "every route multiplies the same bit-exact dequantised weight; matmul_4bit takes the fused "
-                    f"MFMA kernel up to {PREFILL_FUSED_MAX_TOKENS} tokens, above it our dequant kernel + hipBLASLt "
+                    f"MFMA kernels up to {fused_max_tokens(4096)} tokens ({fused_max_tokens(1024)} for 1024 or "
+                    f"14336 rows), above it our dequant kernel + hipBLASLt "
                     "(the reference's F.linear route) unless QZ_PREFILL_GEMM16=1 selects our 8-phase MFMA GEMM "
                     f"(qz_gemm_16bit, >= {GEMM16_MIN_TILES} 256x256 tiles)"}
 

@@ -460,12 +460,21 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
 # PREFILL_GEMM16 (env QZ_PREFILL_GEMM16=1) and >= GEMM16_MIN_TILES 256 x 256
 # output tiles, our staggered 8-phase MFMA GEMM (qz_gemm_16bit); "gemm16"
 # forces the latter where it applies.  "auto" takes the fused kernel up to
-# PREFILL_FUSED_MAX_TOKENS tokens and the dequant route above it (DESIGN.md
+# fused_max_tokens(M) tokens and the dequant route above it (DESIGN.md
 # section 4.2 has the measured crossovers: hipBLASLt is 12-17 % faster than
 # qz_gemm_16bit at T >= 4096 today, so it stays the default).
 PREFILL_FUSED_MAX_TOKENS = int(os.environ.get("QZ_PREFILL_FUSED_MAX_T", "512"))
 PREFILL_GEMM16 = os.environ.get("QZ_PREFILL_GEMM16", "0") == "1"
 GEMM16_MIN_TILES = int(os.environ.get("QZ_GEMM16_MIN_TILES", "256"))
+
+
+def fused_max_tokens(M: int) -> int:
+    """Largest token count the auto route sends to the fused kernels for an M-row
+    weight: the measured crossover against dequantize_4bit + hipBLASLt, whole routes
+    (scripts/prefill_lowT_sweep.py, profiles/r2_prefill_lowT_sweep.txt; Llama-3-8B
+    shapes): 256 tokens for 2048..8192 rows (4096x4096, 4096x14336), 128 otherwise
+    (1024x4096, 14336x4096); never above PREFILL_FUSED_MAX_TOKENS."""
+    return min(PREFILL_FUSED_MAX_TOKENS, 256 if 2048 <= M <= 8192 else 128)
 
 
 def gemm_16bit(A: Tensor, W: Tensor, bias: Optional[Tensor] = None) -> Optional[Tensor]:
@@ -520,7 +529,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
     if route == "fused" and not fused_ok:
         raise ValueError("gemm_4bit: the fused kernel needs fp16/bf16 activations, K % 64 == 0, M % 4 == 0 "
                          "and blocksize >= 64")
-    if fused_ok and (route == "fused" or (route == "auto" and T <= PREFILL_FUSED_MAX_TOKENS)):
+    if fused_ok and (route == "fused" or (route == "auto" and T <= fused_max_tokens(M))):
         out = torch.empty((T, M), dtype=A.dtype, device=A.device)
         if bias is not None and bias.dtype != A.dtype:
             bias = bias.to(A.dtype)

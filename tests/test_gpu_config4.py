@@ -44,7 +44,7 @@ def _layer(M, K, seed):
 
 @pytest.mark.parametrize("M,K", [(4096, 4096), (14336, 4096), (4096, 14336)])
 def test_config4_prefill_T16384_both_routes(M, K):
-    from quantizations_amd.core import PREFILL_FUSED_MAX_TOKENS, gemm_4bit
+    from quantizations_amd.core import fused_max_tokens, gemm_4bit
 
     m, wd = _layer(M, K, seed=M + K)
     g = torch.Generator(device="cuda").manual_seed(2)
@@ -52,7 +52,7 @@ def test_config4_prefill_T16384_both_routes(M, K):
     ref = X.reshape(-1, K).double() @ wd.double().t()               # [16384, M] fp64
     y_auto = m(X)                                                   # product route (modules.py:62-64)
     assert y_auto.shape == (8, 2048, M) and y_auto.dtype == torch.float16
-    assert 16384 > PREFILL_FUSED_MAX_TOKENS                         # auto = dequant + library GEMM here
+    assert 16384 > fused_max_tokens(M)                              # auto = dequant + library GEMM here
     _assert_close_dev(y_auto.reshape(-1, M), ref, f"Linear4bit auto {M}x{K}")
     del y_auto
     y_fused = gemm_4bit(X, m.weight, m.weight.quant_state, route="fused")   # 256 x 256 MFMA tile kernel
@@ -63,7 +63,7 @@ def test_config4_prefill_T16384_both_routes(M, K):
 @pytest.mark.parametrize("T", [513, 2048])
 @pytest.mark.parametrize("M,K", [(4096, 4096), (1024, 4096)])
 def test_linear4bit_prefill_above_fused_threshold(T, M, K):
-    """Linear4bit's auto route just above PREFILL_FUSED_MAX_TOKENS (513) and at
+    """Linear4bit's auto route above the fused crossover (fused_max_tokens: 256 / 128) and at
     one sequence of config #4 (2048), and the fused kernel at the same T."""
     from quantizations_amd.core import gemm_4bit
 

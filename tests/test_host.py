@@ -163,3 +163,13 @@ def test_fuse_layer_ops_leaves_other_rotary_forms_alone():
     finally:
         for modname, _ in created:
             sys.modules.pop(modname, None)
+
+
+def test_fused_route_threshold_follows_measured_crossover():
+    # scripts/prefill_lowT_sweep.py on one MI355X (profiles/r2_prefill_lowT_sweep.txt)
+    from quantizations_amd import core
+
+    assert core.fused_max_tokens(4096) == 256        # 4096x4096, 4096x14336: fused wins to T = 256
+    assert core.fused_max_tokens(1024) == 128        # k/v projections: to T = 128
+    assert core.fused_max_tokens(14336) == 128       # gate/up: a tie at T = 128, dequant route above
+    assert all(core.fused_max_tokens(m) <= core.PREFILL_FUSED_MAX_TOKENS for m in (8, 4096, 1 << 20))

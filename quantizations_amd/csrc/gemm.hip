@@ -534,7 +534,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_big(GemmParams p) {
 // profiles/r2_gemm_mfma32.txt); 16 = no DMA at all and 32 = every step DMAs the k-slice of step 0
 // (microbenchmark timing only: the LDS -> MFMA skeleton, and the schedule with L2-resident
 // operands); 64 = grouped (4 token x 8 row tiles per XCD) tile order; 128 = plain W staged
-// through registers.
+// through registers; 256 = plain W in three buffers, staged two steps ahead one piece per phase.
 // V (microbenchmark A/B, timing only except 0, 2 and 5): 0 = product; 1 = no decode
 // (packed bytes copied); 2 = no group stagger; 3 = as 1 without the W/scale DMAs;
 // 4 = as 3 without the X DMAs (the LDS -> MFMA skeleton alone); 5 = a plain fp16 GEMM on the
@@ -556,7 +556,9 @@ constexpr int k8pX = 0, k8pW = 2 * kBigStage, k8pWp = 4 * kBigStage, k8pSc = k8p
 constexpr int k8pCode2 = k8pSc + 2 * 2048;
 template <int QT, bool DQ, int DT, int V = 0, int SK = 0>
 __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[k8pCode2 + (DQ ? 1024 : 0)];
+  // SK & 256 (plain W): three W buffers (k8pW .. 160 KiB, over the unused packed-W/scale rings)
+  constexpr bool kW3 = V == kPlainW && (SK & 256) != 0;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kW3 ? 163840 : k8pCode2 + (DQ ? 1024 : 0)];
   typedef __attribute__((address_space(3))) void *lds_ptr_t;
   typedef __attribute__((address_space(1))) void *glb_ptr_t;
   float *s_code2 = reinterpret_cast<float *>(smem + k8pCode2);
@@ -621,12 +623,14 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     for (int i = 0; i < 4; ++i)
       *reinterpret_cast<v4u *>(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024 + lane * 16) = wreg[i];
   };
-  auto stage_wf = [&](int step, int buf) {
+  auto stage_wf_piece = [&](int step, int buf, int i) {
     if constexpr ((SK & 16) != 0) return;
+    __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + woff[i] + (uint32_t)step * kStepB),
+                                     (lds_ptr_t)(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
+  };
+  auto stage_wf = [&](int step, int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((glb_ptr_t)(p.B + woff[i] + (uint32_t)step * kStepB),
-                                       (lds_ptr_t)(smem + k8pW + buf * kBigStage + (8 * i + wave) * 1024), 16, 0, 0);
+    for (int i = 0; i < 4; ++i) stage_wf_piece(step, buf, i);
   };
   const int wr = tid >> 1, wh = tid & 1;  // decode ownership: row wr, 32-code half wh
   const int wrow = min(m0 + wr, p.M - 1);
@@ -801,6 +805,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
   __syncthreads();
   if constexpr (V == kPlainW) {
     stage_wf(0, 0);
+    if constexpr (kW3) {
+      if (nsteps > 1) stage_wf(1, 1);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     uint32_t t[8];
@@ -827,8 +834,11 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
 #endif
   // A phase: [read segment: LDS reads + DMA issue only, no waits] s_barrier [lgkmcnt(0);
   // 16 MFMAs with this phase's share of the W(s+1) decode interleaved] s_barrier.
+  int wb3 = 0;  // kW3: W buffer of step s (s % 3)
   for (int s = 0; s < nsteps; ++s) {
     const int b = s & 1;
+    const int wb = kW3 ? wb3 : b;
+    const int wb2 = kW3 ? (wb3 == 0 ? 2 : wb3 - 1) : 0;  // kW3: buffer of step s + 2
     const bool dma = s + 2 < nsteps;    // stage X(s+2) (into this step's buffer, quarter by quarter as
                                         // its last reader passes) and W(s+2)'s packed bytes + scales
     const int ps = (s + 1) & 1;         // ring slot of W(s+1)'s packed bytes
@@ -844,9 +854,11 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
       w0 = read_packed(ps, 0);
     }
     if constexpr (V >= 3) sw.q = sw.q & 0u;
-    load_w(b, 0);
+    load_w(wb, 0);
     load_x(b, 0);
-    if constexpr (V == kPlainW && (SK & 128) != 0) {
+    if constexpr (kW3) {
+      if (dma) stage_wf_piece(s + 2, wb2, 0);       // W(s+2): one piece per phase
+    } else if constexpr (V == kPlainW && (SK & 128) != 0) {
       load_wf_regs(min(s + 1, nsteps - 1));         // written in phase 2 (stale in the last step)
     } else if constexpr (V == kPlainW) {
       if (s + 1 < nsteps) stage_wf(s + 1, b ^ 1);  // retired by this step's phase-3 vmcnt(4)
@@ -870,10 +882,11 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
       w1 = read_packed(ps, 1);
       w2 = read_packed(ps, 2);
     }
-    load_w(b, 1);
+    load_w(wb, 1);
     if (dma) {  // quarters 0 (group 0, tokens lo) and 2 (group 1, tokens lo): last read in phase 0
       stage_xq(s + 2, b, 0);
       stage_xq(s + 2, b, 2);
+      if constexpr (kW3) stage_wf_piece(s + 2, wb2, 1);
     }
     __builtin_amdgcn_s_barrier();
     QZ_ST8(3);
@@ -890,6 +903,9 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     // ---------------- phase 2: (rows hi, tokens hi) ----------------
     if constexpr (V != kPlainW) w3 = read_packed(ps, 3);
     load_x(b, 1);
+    if constexpr (kW3) {
+      if (dma) stage_wf_piece(s + 2, wb2, 2);
+    }
     __builtin_amdgcn_s_barrier();
     QZ_ST8(5);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -906,14 +922,20 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     QZ_ST8(6);
     __builtin_amdgcn_s_barrier();
     // ---------------- phase 3: (rows lo, tokens hi); retire the step's staging ----------------
-    if constexpr ((SK & 1) == 0) load_w(b, 0);
+    if constexpr ((SK & 1) == 0) load_w(wb, 0);
     if (dma) {  // quarters 1 and 3 (tokens hi): last read in phase 2
       stage_xq(s + 2, b, 1);
       stage_xq(s + 2, b, 3);
+      if constexpr (kW3) stage_wf_piece(s + 2, wb2, 3);
     }
     // retire X(s+1) and W(s+2)'s bytes; X(s+2)'s four quarter DMAs may stay in flight
-    if (dma) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (kW3: W is staged two steps ahead too: this step's 8 DMAs stay in flight)
+    if (dma) {
+      if constexpr (kW3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     QZ_ST8(7);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -923,6 +945,7 @@ __global__ __launch_bounds__(512) void k_gemm_4bit_8p(GemmParams p) {
     if constexpr ((SK & 6) == 0) __builtin_amdgcn_s_setprio(0);
     QZ_ST8(8);
     __builtin_amdgcn_s_barrier();
+    wb3 = wb3 == 2 ? 0 : wb3 + 1;
   }
   if (V != 2 && wt == 0) __builtin_amdgcn_s_barrier();  // matches group 1's extra barrier
 #ifdef QZ_STAMPS8P

@@ -64,7 +64,7 @@ def log(*a):
 
 
 def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_type: str = "nf4",
-                double_quant: bool = True):
+                double_quant: bool = True, dtype: torch.dtype = torch.float16):
     from transformers import LlamaConfig, LlamaForCausalLM
 
     from quantizations_amd.integration import replace_with_bnb_linear
@@ -73,7 +73,7 @@ def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_typ
     cfg = LlamaConfig(**{**base, "num_hidden_layers": layers or base["num_hidden_layers"]})
     torch.manual_seed(seed)
     prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.float16)
+    torch.set_default_dtype(dtype)
     with torch.device("cuda"):
         model = LlamaForCausalLM(cfg)
     torch.set_default_dtype(prev)
@@ -641,6 +641,8 @@ def main():
                     help="llama3-8b (configs #1-#4) or llama3-70b (config #5)")
     ap.add_argument("--quant", choices=("nf4", "fp4"), default="nf4", help="codebook (config #3: fp4 --no-dq)")
     ap.add_argument("--no-dq", action="store_true", help="fp32 absmax instead of double quant")
+    ap.add_argument("--dtype", choices=("fp16", "bf16"), default="fp16",
+                    help="model / activation dtype (bf16: SURVEY 8(f) row 4, the bf16 activation path)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the decode step")
     ap.add_argument("--no-roofline", action="store_true")
@@ -704,7 +706,8 @@ def main():
     def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int):
         t_build = time.perf_counter()
         model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
-                                 double_quant=not args.no_dq)
+                                 double_quant=not args.no_dq,
+                                 dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
                                                      layer_ops=layer_ops)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
@@ -804,10 +807,13 @@ def main():
                        f"{args.quant.upper()} bs=1; 4096×4096 GEMV GB/s vs HBM peak"),
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": f"f16 activations x 4-bit {args.quant.upper()} weights, fp32 accumulate",
+            "scaling": "weak" if weak else "strong", "vs_baseline": None,
+            "dtype": f"{'bf16' if args.dtype == 'bf16' else 'f16'} activations x 4-bit {args.quant.upper()} weights, "
+                     "fp32 accumulate",
             "data": f"synthetic (random-init {'Llama-3-70B' if args.model == 'llama3-70b' else 'Llama-3-8B'} "
                     "architecture, random prompt)",
-            "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}-decode-bs1",
+            "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}"
+                                   f"{'-bf16' if args.dtype == 'bf16' else ''}-decode-bs1",
                        "layers": cfg.num_hidden_layers,
                        "prompt_len": args.prompt, "global_batch": gbatch, "streams_per_gpu": gbatch / world,
                        "stream_batch": 1, "decode": mode,

@@ -135,13 +135,42 @@ constexpr ByteTable make_nf4_exact_table() {
   }
   return t;
 }
+// bf16 activations (round 2): the codes as bf16 hi + lo pairs -- c = hi + lo to ~2^-16 --
+// dotted straight against the raw bf16 x pairs with v_dot2c_f32_bf16 (no x conversion, no
+// pre-scale: bf16 has fp32's exponent range).  Entries {hi pair, lo pair}, the CL geometry.
+constexpr uint16_t bf16_bits_rne_c(float f) {  // finite values
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+constexpr float bf16_value_c(uint16_t b) { return __builtin_bit_cast(float, (uint32_t)b << 16); }
+constexpr ByteTable make_bf16_table(const float (&c)[16]) {
+  uint16_t hi[16] = {}, lo[16] = {};
+  for (int i = 0; i < 16; ++i) {
+    hi[i] = bf16_bits_rne_c(c[i]);
+    lo[i] = bf16_bits_rne_c(c[i] - bf16_value_c(hi[i]));        // the residual is exact in fp32
+  }
+  ByteTable t{};
+  for (int e = 0; e < 256; ++e) {
+    const uint32_t h = (uint32_t)hi[e >> 4] | ((uint32_t)hi[e & 15] << 16);
+    const uint32_t l = (uint32_t)lo[e >> 4] | ((uint32_t)lo[e & 15] << 16);
+    t.v[4 * e + 0] = h; t.v[4 * e + 1] = l; t.v[4 * e + 2] = h; t.v[4 * e + 3] = l;
+  }
+  return t;
+}
+// FP4 x12 magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3} are exact in bf16 (lo = 0); out_scale 1/12
+constexpr float kFP4x12Host[16] = {0.0f, 0.0625f, 8.0f, 12.0f, 4.0f, 6.0f, 2.0f, 3.0f,
+                                   -0.0f, -0.0625f, -8.0f, -12.0f, -4.0f, -6.0f, -2.0f, -3.0f};
 __device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
 __device__ const ByteTable g_byte_tab_nf4x = make_nf4_exact_table();
 __device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
+__device__ const ByteTable g_byte_tab_nf4_bf = make_bf16_table(kNF4Host);
+__device__ const ByteTable g_byte_tab_fp4_bf = make_bf16_table(kFP4x12Host);
+static_assert(bf16_bits_rne_c(0.07958029955625534f) == 0x3DA3, "bf16 RNE of an NF4 code");
 static_assert(f16_bits_rne_c(0.07958029955625534f) == 0x2D18, "fp16 RNE of an NF4 code");
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 struct GemvParams {
   const unsigned char *B;
@@ -282,7 +311,13 @@ __device__ __forceinline__ void decode_lut16(uint32_t w, const uint32_t (&t)[8],
 // 16 half2 "hi" (+ "lo" for fp32/bf16 activations) in the pair order of MODE
 // only at compute time.
 template <int MODE, int DT> struct XSlice {
-  static constexpr bool kSplit = DT != QZ_DT_F16;
+  // fp32 x needs the lo part; a bf16 value (8-bit significand) pre-scaled into fp16's range is
+  // exact in the hi part, and whatever it loses below fp16's smallest subnormal its lo part
+  // (rtz of a residual < 2^-24) loses too: bf16 lo is identically zero, so it is not formed
+  static constexpr bool kSplit = DT == QZ_DT_F32;
+  // the byte-table decode dots bf16 x raw against bf16 code pairs (kBF): no conversion at all
+  static constexpr bool kRawBF = DT == QZ_DT_BF16 && MODE == kModeTab;
+  static constexpr bool kScaled = DT != QZ_DT_F16 && !kRawBF;
   static constexpr int kWords = DT == QZ_DT_F32 ? 32 : 16;  // raw dwords per lane
   uint32_t raw[kWords];
 
@@ -310,7 +345,10 @@ template <int MODE, int DT> struct XSlice {
   // never saturates, lo never flushes); usc = 2^-se undoes it on the dot.
   __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1], float &usc) const {
     usc = 1.0f;
-    if constexpr (DT == QZ_DT_F16) {
+    if constexpr (kRawBF) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) hi[i] = raw[i];
+    } else if constexpr (DT == QZ_DT_F16) {
       if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) hi[i] = raw[i];
@@ -357,9 +395,11 @@ template <int MODE, int DT> struct XSlice {
           // hi = rtz(f s) (|f s| < 2^15), lo = rtz(f s - hi); f s - hi is exact
           const float fa = f[8 * d + a[j]] * sc, fb = f[8 * d + b[j]] * sc;
           const auto h = __builtin_amdgcn_cvt_pkrtz(fa, fb);
-          const float ra = fa - (float)h.x, rb = fb - (float)h.y;
           hi[4 * d + j] = __builtin_bit_cast(uint32_t, h);
-          lo[4 * d + j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(ra, rb));
+          if constexpr (kSplit) {
+            const float ra = fa - (float)h.x, rb = fb - (float)h.y;
+            lo[4 * d + j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(ra, rb));
+          }
         }
       }
     }
@@ -401,10 +441,11 @@ __device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)
 // byte value, so the address of byte m is (byte << 7) | jb either way.
 // (ABL: benchmark-only ablations -- 16 replaces the dot products by integer
 // adds, 32 replaces the table reads by the addresses themselves.)
-template <bool SPLIT, int ABL = 0, bool CL = false, bool WT = false>
+template <bool SPLIT, int ABL = 0, bool CL = false, bool WT = false, bool BF = false>
 __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&hi)[16],
                                                const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t *s_tab,
                                                uint32_t jb) {
+  static_assert(!BF || CL, "bf16 entries use the 64-bit (CL) table geometry");
   const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
   const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
   uint32_t v[16], vl[CL ? 16 : 1];
@@ -449,6 +490,13 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     float &acc = (i & 1) ? s1 : s0;
+    if constexpr (BF) {  // bf16 code pairs (hi, lo) against the raw bf16 x pair
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, v[i]), __builtin_bit_cast(bf16x2_t, hi[i]),
+                                            acc, false);
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, vl[i]), __builtin_bit_cast(bf16x2_t, hi[i]),
+                                            acc, false);
+      continue;
+    }
     acc = dot2(v[i], hi[i], acc);
     if constexpr (CL) acc = dot2(vl[i], hi[i], acc);   // code residual x x_hi
     if constexpr (SPLIT) acc = dot2(v[i], lo[i], acc);  // code_hi x x residual
@@ -529,6 +577,20 @@ __device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const fl
     const float ra = ca - (float)__builtin_bit_cast(_Float16, (uint16_t)(h & 0xFFFFu));
     const float rb = cb - (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> 16));
     const uint32_t l = cvt_pk_f16_rne(ra, rb);
+    store_byte_table_entry<PIECES>(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
+  }
+}
+
+// Builds the bf16 byte table from a runtime fp32 codebook: entry e = {hi pair, lo pair} of
+// (code[e >> 4], code[e & 15]) as bf16 hi + lo (c = hi + lo to ~2^-16), 16 copies.
+template <int NT, int PIECES = kTabCopies / 4>
+__device__ __forceinline__ void build_byte_table_bf16(uint32_t *s_tab, const float *lut) {
+  for (int e = threadIdx.x; e < 256; e += NT) {
+    const float ca = lut[e >> 4], cb = lut[e & 15];
+    const uint32_t ha = __builtin_bit_cast(uint16_t, (__bf16)ca), hb = __builtin_bit_cast(uint16_t, (__bf16)cb);
+    const float ra = ca - __builtin_bit_cast(float, ha << 16), rb = cb - __builtin_bit_cast(float, hb << 16);
+    const uint32_t la = __builtin_bit_cast(uint16_t, (__bf16)ra), lb = __builtin_bit_cast(uint16_t, (__bf16)rb);
+    const uint32_t h = ha | (hb << 16), l = la | (lb << 16);
     store_byte_table_entry<PIECES>(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
   }
 }
@@ -628,7 +690,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   QZ_STAMP(0);
   const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
-  constexpr bool kSplit = DT != QZ_DT_F16;
+  constexpr bool kSplit = XSlice<MODE, DT>::kSplit;   // fp32 x: hi + lo parts
+  // bf16 x (byte-table decode): bf16 code pairs hi + lo in 64-bit entries, the CL geometry
+  constexpr bool kBF = XSlice<MODE, DT>::kRawBF;
+  constexpr bool kWide = CL || kBF;
+  constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[DQ ? 256 : 1];
   __shared__ float s_part[NW][R];
@@ -659,7 +725,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
     if (!p.lut && threadIdx.x < 256) {
-      const ByteTable *bt = CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4);
+      const ByteTable *bt = kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
+                                : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
       tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
     }
   }
@@ -709,7 +776,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // runtime codebook (always exact codes) 2^-S of its in-kernel split
   float out_scale = p.out_scale;
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if constexpr (CL) {
+    if constexpr (kBF) {
+      if (p.lut) {
+        out_scale = 1.0f;
+        build_byte_table_bf16<NW * 64, kPieces>(s_tab, p.lut);
+      } else if (threadIdx.x < 256) {
+        store_byte_table_entry<kPieces>(s_tab, tab_entry);
+      }
+    } else if constexpr (CL) {
       if (p.lut) {
         const int S = lut_shift(p.lut);
         out_scale = ldexpf(1.0f, -S);
@@ -724,8 +798,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   }
   if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
   QZ_STAMP(1);
-  const uint32_t jb = WT ? (CL ? (uint32_t)(lane & 31) << 3 : (uint32_t)lane << 2)
-                        : (CL ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2);
+  const uint32_t jb = WT ? (kWide ? (uint32_t)(lane & 31) << 3 : (uint32_t)lane << 2)
+                        : (kWide ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2);
 
   float acc[R];
 #pragma unroll
@@ -747,9 +821,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
       else am = c.a[r];
       am = c.on ? am : 0.0f;
-      if constexpr (kSplit) am *= usc;  // exact: a power of two (the lane's x pre-scale)
+      if constexpr (kScaled) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
-      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, CL, WT>(c.wv[r], hi, lo, s_tab, jb);
+      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
     }
@@ -1016,8 +1090,14 @@ static bool full_steps(int K, int blocksize, int blocksize2, bool dq, long long 
 // Decode tables for the byte-table kernel: the 16-entry codebook as fp16 byte
 // planes (a runtime `lut` is converted in kernel, so its planes stay zero).
 // Exact codes (CL): the built-in NF4 table holds code * 2^14 as hi + lo.
-static void set_tables(int quant_type, const float *lut, bool cl, GemvParams *p) {
+static void set_tables(int quant_type, const float *lut, bool cl, int dtype, GemvParams *p) {
   build_tables(kModeTab, lut ? QZ_NF4 : quant_type, p->tab, &p->out_scale);
+  if (dtype == QZ_DT_BF16) {  // bf16 code tables: true NF4 codes, FP4 x12; a runtime book in kernel
+    const bool fp4 = !lut && quant_type == QZ_FP4;
+    p->tabsel = fp4 ? 1 : 0;
+    p->out_scale = fp4 ? 1.0f / 12.0f : 1.0f;
+    return;
+  }
   p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : (cl ? 2 : 0);
   if (lut) p->out_scale = 1.0f;
   else if (cl) p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
@@ -1077,7 +1157,8 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   if (M == 0) return QZ_OK;
   const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
-  const bool cl = exact_codes(quant_type, lut);
+  // bf16 x always decodes with bf16 hi + lo codes (~2^-16): no separate exact-code table
+  const bool cl = exact_codes(quant_type, lut) && dtype != QZ_DT_BF16;
   quant_type &= ~QZ_EXACT_CODES;
 
   if (!vec_ok) {
@@ -1097,7 +1178,7 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
 
   int R, WK;
   choose_geometry(M, K, &R, &WK);
-  set_tables(quant_type, lut, cl, &p);
+  set_tables(quant_type, lut, cl, dtype, &p);
   const bool fs = full_steps(K, blocksize, blocksize2, dq, block_base);
   const int rc = cl ? dispatch_tab<true>(p, dtype, dq, fs, R, WK, s) : dispatch_tab<false>(p, dtype, dq, fs, R, WK, s);
   if (rc != QZ_OK) return rc;
@@ -1110,7 +1191,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
   GemvGroup g;
   g.nseg = nseg;
-  const bool cl = exact_codes(quant_type, lut);
+  const bool cl = exact_codes(quant_type, lut) && dtype != QZ_DT_BF16;
   bool all_vec = true;
   long long total_m = 0;
   const bool dq = segs[0].qabsmax != nullptr;
@@ -1139,7 +1220,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
-    set_tables(quant_type & ~QZ_EXACT_CODES, lut, cl, &g.seg[i]);
+    set_tables(quant_type & ~QZ_EXACT_CODES, lut, cl, dtype, &g.seg[i]);
     g.start[i] = blocks;
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }

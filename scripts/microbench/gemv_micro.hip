@@ -321,6 +321,15 @@ int main(int argc, char **argv) {
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
     const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
     hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, ABL, true>), dim3(g), dim3(256), 0, 0, q); })
+#define GVB(R, DT_, NAME) timeit("gemvFS tab dq R=" #R " x=" NAME, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, DT_, R, 1, 4, false, 0, true>), dim3(g), dim3(256), 0, 0, q); })
+  const bool bf16 = argc > 4 && std::string(argv[4]) == "bf16";
+  if (bf16) {  // activation dtype: rows per wave for bf16 x (its per-lane convert is shared by R rows)
+    GVB(2, QZ_DT_F16, "f16"); GVB(4, QZ_DT_F16, "f16");
+    GVB(1, QZ_DT_BF16, "bf16"); GVB(2, QZ_DT_BF16, "bf16"); GVB(4, QZ_DT_BF16, "bf16");
+  }
   const bool xcopy = argc > 4 && std::string(argv[4]) == "xcopy";
   if (xcopy) {  // x hot-spot test: every wave reads its own copy of x (ABL 2048)
     GVFS(2, 0); GVFS(2, 2048); GVFS(4, 0); GVFS(4, 2048); GVFS(1, 0); GVFS(1, 2048);
@@ -349,7 +358,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

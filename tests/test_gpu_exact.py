@@ -146,3 +146,35 @@ def test_gemv_activation_mixed_magnitudes(orc, dt):
     y = gemv_4bit(x.to(DEV).reshape(1, K), packed, state=st, exact_codes=True).double().cpu().numpy().ravel()
     tol = EXACT_TOL if dt == torch.float32 else 2.0 ** -8
     assert _rel(y, yref) <= tol
+
+
+@pytest.mark.parametrize("quant_type", ["nf4", "fp4"])
+@pytest.mark.parametrize("scale", [1.0, 1e-30, 1e30])
+def test_bf16_activations_raw_bf16_codes(orc, quant_type, scale):
+    """bf16 activations are dotted raw against bf16 hi + lo code pairs (v_dot2c_f32_bf16, no
+    x conversion or pre-scale): against the fp64 product of the same bf16 x with the oracle's
+    fp32 weight products, within the bf16 output's own rounding at any magnitude, single and
+    grouped launches; exact_codes does not change the bf16 table."""
+    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, quantize_4bit
+
+    M, K = 1024, 4096
+    W = _weights(M, K, seed=31)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=quant_type)
+    o = orc.quantize_4bit(W.float().numpy(), 64, quant_type)
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn(K, generator=g).double() * scale
+    x[::61] *= 3e3
+    x[512:576] = 0.0
+    xb = x.to(torch.bfloat16)
+    yref = orc.gemv(xb.double().numpy(), o)
+    y = gemv_4bit(xb.to(DEV).reshape(1, K), packed, state=st)
+    assert y.dtype == torch.bfloat16
+    yd = y.double().cpu().numpy().ravel()
+    assert np.all(np.isfinite(yd))
+    assert _rel(yd, yref) <= 2.0 ** -8
+    # elementwise: one bf16 rounding of the result (2^-8 relative) + fp32-class noise of the sum
+    assert np.all(np.abs(yd - yref) <= 2.0 ** -8 * np.abs(yref) + 1e-5 * np.abs(yref).max())
+    assert torch.equal(gemv_4bit(xb.to(DEV).reshape(1, K), packed, state=st, exact_codes=True), y)
+    ys = gemv_4bit_grouped(xb.to(DEV).reshape(1, K), [(packed, st, None), (packed, st, None)])
+    assert torch.equal(ys[0], ys[1])      # (its geometry may split K unlike the single launch)
+    assert _rel(ys[0].double().cpu().numpy().ravel(), yref) <= 2.0 ** -8

@@ -172,6 +172,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
+// two outputs in the 16-bit format of DT, element 0 in the low half (each converted exactly as
+// store_f32 converts it)
+template <int DT> __device__ __forceinline__ uint32_t pack16(float a, float b) {
+  if constexpr (DT == QZ_DT_F16) {
+    return (uint32_t)f32_to_f16_bits(a) | ((uint32_t)f32_to_f16_bits(b) << 16);
+  } else {
+    return (uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(a)) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, __float2bfloat16(b)) << 16);
+  }
+}
+
 struct GemvParams {
   const unsigned char *B;
   const void *x;
@@ -869,16 +880,31 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = (ABL & 8) ? acc[r] : wave_sum_last(acc[r]);
     if (lane == kWave - 1) {
+      // 16-bit outputs of a row pair inside M go out as one dword (row0 is even for even R)
+      constexpr bool kPack = DT != QZ_DT_F32 && R % 2 == 0 && (ABL & (1024 | 4096)) == 0;  // 4096: A/B knob
+      const bool pack = kPack && row0 + R <= p.M && (reinterpret_cast<uintptr_t>(p.y) & 3u) == 0;
+      if (pack) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int row = row0 + r;
-        if (row < p.M) {
-          float o = v[r] * out_scale;
-          if (p.bias) o += load_f32<DT>(p.bias, row);
-          if constexpr ((ABL & 1024) != 0 && DT == QZ_DT_F16)  // microbenchmark: non-temporal y store
-            __builtin_nontemporal_store((uint16_t)f32_to_f16_bits(o), reinterpret_cast<uint16_t *>(p.y) + row);
-          else
-            store_f32<DT>(p.y, row, o);
+        for (int r = 0; r < R; r += 2) {
+          float o0 = v[r] * out_scale, o1 = v[r + 1] * out_scale;
+          if (p.bias) {
+            o0 += load_f32<DT>(p.bias, row0 + r);
+            o1 += load_f32<DT>(p.bias, row0 + r + 1);
+          }
+          reinterpret_cast<uint32_t *>(p.y)[(row0 + r) >> 1] = pack16<DT>(o0, o1);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int row = row0 + r;
+          if (row < p.M) {
+            float o = v[r] * out_scale;
+            if (p.bias) o += load_f32<DT>(p.bias, row);
+            if constexpr ((ABL & 1024) != 0 && DT == QZ_DT_F16)  // microbenchmark: non-temporal y store
+              __builtin_nontemporal_store((uint16_t)f32_to_f16_bits(o), reinterpret_cast<uint16_t *>(p.y) + row);
+            else
+              store_f32<DT>(p.y, row, o);
+          }
         }
       }
     }

@@ -330,6 +330,10 @@ int main(int argc, char **argv) {
     GVB(2, QZ_DT_F16, "f16"); GVB(4, QZ_DT_F16, "f16");
     GVB(1, QZ_DT_BF16, "bf16"); GVB(2, QZ_DT_BF16, "bf16"); GVB(4, QZ_DT_BF16, "bf16");
   }
+  const bool pk = argc > 4 && std::string(argv[4]) == "pack";
+  if (pk) {  // y stores: packed row pairs (product) vs one 16-bit store per row (ABL 4096)
+    GVFS(2, 0); GVFS(2, 4096); GVFS(4, 0); GVFS(4, 4096);
+  }
   const bool xcopy = argc > 4 && std::string(argv[4]) == "xcopy";
   if (xcopy) {  // x hot-spot test: every wave reads its own copy of x (ABL 2048)
     GVFS(2, 0); GVFS(2, 2048); GVFS(4, 0); GVFS(4, 2048); GVFS(1, 0); GVFS(1, 2048);
@@ -358,7 +362,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

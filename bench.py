@@ -320,14 +320,13 @@ GEMV_EXTRA = {}
 
 @torch.inference_mode()
 def gemv_parity():
-    """Decode-GEMV accuracy at the Llama-3-8B shapes (NF4 + double quant, fp16 x):
-    rel err ||y - y_ref|| / ||y_ref|| with y_ref the fp64 product of the fp32
+    """Decode-GEMV accuracy at the Llama-3-8B shapes (NF4 + double quant): rel err
+    ||y - y_ref|| / ||y_ref|| with y_ref the fp64 product of the same x with the fp32
     dequantised weight (= the reference's fp32 weight products kernels.cu:1169;
-    dequantize_4bit(fp32) is pinned bit-exact to the oracle in tests/), for the
-    default fp16-code table and the exact-code variant; fp16 output (the bench
-    config) and fp32 output (x in fp32: the code error is not hidden by the
-    output rounding)."""
-    from quantizations_amd import _lib
+    dequantize_4bit(fp32) is pinned bit-exact to the oracle in tests/).  Each activation
+    dtype has its own code table: fp16 x the fp16-rounded codes (default) or the exact
+    hi + lo codes; bf16 x bf16 hi + lo codes; fp32 x the fp32 codes.  Outputs are in x's
+    dtype, so the fp16/bf16 figures include the output's own rounding."""
     from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
 
     dev = torch.device("cuda")
@@ -338,22 +337,21 @@ def gemv_parity():
         packed, st = quantize_4bit(W, quant_type="nf4")
         del W
         wd = dequantize_4bit(packed, st, out_dtype=torch.float32).t().double()   # [M, K]
-        x = torch.randn(K, device=dev).half()
-        ref = wd @ x.double()
+        x = torch.randn(K, device=dev)
         row = {}
-        for name, ex in (("fp16_codes", False), ("exact_codes", True)):
-            for xdt in (torch.float16, torch.float32):
-                y = gemv_4bit(x.to(xdt).reshape(1, K), packed, state=st, exact_codes=ex).reshape(-1).double()
-                row[f"{name}_{'f16' if xdt == torch.float16 else 'f32'}_out"] = \
-                    float(f"{((y - ref).norm() / ref.norm()).item():.3e}")
+        for name, xdt, ex in (("fp16_codes_f16", torch.float16, False), ("exact_codes_f16", torch.float16, True),
+                              ("bf16_codes_bf16", torch.bfloat16, None), ("fp32_codes_f32", torch.float32, None)):
+            xx = x.to(xdt)
+            ref = wd @ xx.double()
+            y = gemv_4bit(xx.reshape(1, K), packed, state=st, exact_codes=ex).reshape(-1).double()
+            row[name] = float(f"{((y - ref).norm() / ref.norm()).item():.3e}")
         res[f"{M}x{K}"] = row
         del wd, packed, st
-    from quantizations_amd import core
+    from quantizations_amd import _lib, core
     return {"rel_err_vs_fp32_weight_products": res, "tolerance": 1e-3,
             "default": {"f16_activations": "exact_codes" if core._gemv_quant_type("nf4", None, torch.float16)
                         & _lib.EXACT_CODES else "fp16_codes",
-                        "f32_activations": "exact_codes" if core._gemv_quant_type("nf4", None, torch.float32)
-                        & _lib.EXACT_CODES else "fp16_codes"}}
+                        "bf16_activations": "bf16 hi+lo codes", "f32_activations": "fp32 codes"}}
 
 
 def gemv_alg_bytes(shapes, dq: bool = True, x_bytes: int = 2, y_bytes: int = 2) -> int:

@@ -164,7 +164,19 @@ __device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
 __device__ const ByteTable g_byte_tab_nf4x = make_nf4_exact_table();
 __device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
 __device__ const ByteTable g_byte_tab_nf4_bf = make_bf16_table(kNF4Host);
+// fp32 activations (round 2): entries {code[e >> 4], code[e & 15]} as fp32 -- the reference's
+// own fp32 quant_map values (kernels.cu:1115-1120) -- multiplied into the raw fp32 x by v_fma_f32
+constexpr ByteTable make_f32_table(const float (&c)[16]) {
+  ByteTable t{};
+  for (int e = 0; e < 256; ++e) {
+    const uint32_t a = __builtin_bit_cast(uint32_t, c[e >> 4]), b = __builtin_bit_cast(uint32_t, c[e & 15]);
+    t.v[4 * e + 0] = a; t.v[4 * e + 1] = b; t.v[4 * e + 2] = a; t.v[4 * e + 3] = b;
+  }
+  return t;
+}
 __device__ const ByteTable g_byte_tab_fp4_bf = make_bf16_table(kFP4x12Host);
+__device__ const ByteTable g_byte_tab_nf4_f32 = make_f32_table(kNF4Host);
+__device__ const ByteTable g_byte_tab_fp4_f32 = make_f32_table(kFP4x12Host);
 static_assert(bf16_bits_rne_c(0.07958029955625534f) == 0x3DA3, "bf16 RNE of an NF4 code");
 static_assert(f16_bits_rne_c(0.07958029955625534f) == 0x2D18, "fp16 RNE of an NF4 code");
 
@@ -325,10 +337,12 @@ template <int MODE, int DT> struct XSlice {
   // fp32 x needs the lo part; a bf16 value (8-bit significand) pre-scaled into fp16's range is
   // exact in the hi part, and whatever it loses below fp16's smallest subnormal its lo part
   // (rtz of a residual < 2^-24) loses too: bf16 lo is identically zero, so it is not formed
-  static constexpr bool kSplit = DT == QZ_DT_F32;
-  // the byte-table decode dots bf16 x raw against bf16 code pairs (kBF): no conversion at all
+  // the byte-table decode takes bf16 x raw against bf16 code pairs (kRawBF) and fp32 x raw
+  // against fp32 codes (kRawF32): no conversion at all
   static constexpr bool kRawBF = DT == QZ_DT_BF16 && MODE == kModeTab;
-  static constexpr bool kScaled = DT != QZ_DT_F16 && !kRawBF;
+  static constexpr bool kRawF32 = DT == QZ_DT_F32 && MODE == kModeTab;
+  static constexpr bool kSplit = DT == QZ_DT_F32 && !kRawF32;
+  static constexpr bool kScaled = DT != QZ_DT_F16 && !kRawBF && !kRawF32;
   static constexpr int kWords = DT == QZ_DT_F32 ? 32 : 16;  // raw dwords per lane
   uint32_t raw[kWords];
 
@@ -356,7 +370,9 @@ template <int MODE, int DT> struct XSlice {
   // never saturates, lo never flushes); usc = 2^-se undoes it on the dot.
   __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1], float &usc) const {
     usc = 1.0f;
-    if constexpr (kRawBF) {
+    if constexpr (kRawF32) {
+      return;  // chunk_dot_tab_f32 reads raw[] itself
+    } else if constexpr (kRawBF) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) hi[i] = raw[i];
     } else if constexpr (DT == QZ_DT_F16) {
@@ -515,6 +531,30 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
   return s0 + s1;
 }
 
+// fp32 x (kRawF32): byte m of the lane's chunk holds elements 2m (high nibble) and 2m + 1;
+// its 64-bit entry {code_hi, code_lo} (fp32) goes into two v_fma_f32 with the raw x.  Same
+// 128-B-per-byte-value geometry as the CL table.
+__device__ __forceinline__ float chunk_dot_tab_f32(const u32x4 &wv, const uint32_t (&xr)[32], const uint32_t *s_tab,
+                                                   uint32_t jb) {
+  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
+                           ((w[d] >> 9) & 0x7F80u) | jb, ((w[d] >> 17) & 0x7F80u) | jb};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a[m]);
+      const int k = 2 * (4 * d + m);
+      float &acc = (m & 1) ? s1 : s0;
+      acc = fmaf(__uint_as_float(e.x), __uint_as_float(xr[k]), acc);
+      acc = fmaf(__uint_as_float(e.y), __uint_as_float(xr[k + 1]), acc);
+    }
+  }
+  return s0 + s1;
+}
+
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
 // (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
 // readlane round trips through SGPRs.
@@ -603,6 +643,15 @@ __device__ __forceinline__ void build_byte_table_bf16(uint32_t *s_tab, const flo
     const uint32_t la = __builtin_bit_cast(uint16_t, (__bf16)ra), lb = __builtin_bit_cast(uint16_t, (__bf16)rb);
     const uint32_t h = ha | (hb << 16), l = la | (lb << 16);
     store_byte_table_entry<PIECES>(s_tab, u32x4{h, l, h, l}, (uint32_t)e);
+  }
+}
+
+// The fp32 byte table from a runtime codebook: entry e = {code[e >> 4], code[e & 15]}, 16 copies.
+template <int NT, int PIECES = kTabCopies / 4>
+__device__ __forceinline__ void build_byte_table_f32(uint32_t *s_tab, const float *lut) {
+  for (int e = threadIdx.x; e < 256; e += NT) {
+    const uint32_t a = __float_as_uint(lut[e >> 4]), b = __float_as_uint(lut[e & 15]);
+    store_byte_table_entry<PIECES>(s_tab, u32x4{a, b, a, b}, (uint32_t)e);
   }
 }
 
@@ -704,7 +753,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   constexpr bool kSplit = XSlice<MODE, DT>::kSplit;   // fp32 x: hi + lo parts
   // bf16 x (byte-table decode): bf16 code pairs hi + lo in 64-bit entries, the CL geometry
   constexpr bool kBF = XSlice<MODE, DT>::kRawBF;
-  constexpr bool kWide = CL || kBF;
+  constexpr bool kF32 = XSlice<MODE, DT>::kRawF32;    // fp32 x: fp32 code table, v_fma_f32
+  constexpr bool kWide = CL || kBF || kF32;
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[DQ ? 256 : 1];
@@ -736,8 +786,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
     if (!p.lut && threadIdx.x < 256) {
-      const ByteTable *bt = kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
-                                : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
+      const ByteTable *bt = kF32  ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
+                            : kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
+                                  : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
       tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
     }
   }
@@ -787,7 +838,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // runtime codebook (always exact codes) 2^-S of its in-kernel split
   float out_scale = p.out_scale;
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if constexpr (kBF) {
+    if constexpr (kF32) {
+      if (p.lut) {
+        out_scale = 1.0f;
+        build_byte_table_f32<NW * 64, kPieces>(s_tab, p.lut);
+      } else if (threadIdx.x < 256) {
+        store_byte_table_entry<kPieces>(s_tab, tab_entry);
+      }
+    } else if constexpr (kBF) {
       if (p.lut) {
         out_scale = 1.0f;
         build_byte_table_bf16<NW * 64, kPieces>(s_tab, p.lut);
@@ -834,7 +892,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       am = c.on ? am : 0.0f;
       if constexpr (kScaled) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
-      if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
+      if constexpr (kF32) d = chunk_dot_tab_f32(c.wv[r], c.xs.raw, s_tab, jb);
+      else if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
     }
@@ -1092,11 +1151,15 @@ using namespace qz;
 //  * WK=1 (a wave owns whole rows: no cross-wave reduction), then R halves /
 //    WK doubles until the grid has >= 2048 waves, so small-M slices (TP
 //    shards, 1024-row k/v projections) still fill the 256 CUs.
-static void choose_geometry(int M, int K, int *R, int *WK) {
+//  * fp32 x (128 B of x per lane per step, twice the weight bytes of a row pair): R=4 down to
+//    1024 waves (profiles/r2_gemv_f32_R.txt: 4096^2 6.36 -> 5.87 us, 14336x4096 17.9 -> 13.9).
+static void choose_geometry(int M, int K, int dtype, int *R, int *WK) {
   const int nsteps = ((K >> 1) + 1023) >> 10;
-  *R = ((long long)M * K >= (1LL << 26)) ? 4 : 2;
+  const bool f32 = dtype == QZ_DT_F32;
+  *R = (f32 || (long long)M * K >= (1LL << 26)) ? 4 : 2;
   *WK = 1;
-  while ((long long)((M + *R - 1) / *R) * (*WK) < 2048) {
+  const long long min_waves = f32 ? 1024 : 2048;
+  while ((long long)((M + *R - 1) / *R) * (*WK) < min_waves) {
     if (*R > 1) *R >>= 1;
     else if (*WK < 4 && *WK * 2 <= nsteps) *WK <<= 1;
     else break;
@@ -1118,7 +1181,7 @@ static bool full_steps(int K, int blocksize, int blocksize2, bool dq, long long 
 // Exact codes (CL): the built-in NF4 table holds code * 2^14 as hi + lo.
 static void set_tables(int quant_type, const float *lut, bool cl, int dtype, GemvParams *p) {
   build_tables(kModeTab, lut ? QZ_NF4 : quant_type, p->tab, &p->out_scale);
-  if (dtype == QZ_DT_BF16) {  // bf16 code tables: true NF4 codes, FP4 x12; a runtime book in kernel
+  if (dtype == QZ_DT_BF16 || dtype == QZ_DT_F32) {  // bf16 / fp32 code tables: NF4 codes, FP4 x12
     const bool fp4 = !lut && quant_type == QZ_FP4;
     p->tabsel = fp4 ? 1 : 0;
     p->out_scale = fp4 ? 1.0f / 12.0f : 1.0f;
@@ -1183,8 +1246,9 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   if (M == 0) return QZ_OK;
   const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
-  // bf16 x always decodes with bf16 hi + lo codes (~2^-16): no separate exact-code table
-  const bool cl = exact_codes(quant_type, lut) && dtype != QZ_DT_BF16;
+  // bf16 x always decodes with bf16 hi + lo codes (~2^-16) and fp32 x with fp32 codes: the
+  // exact-code (CL) variant is the fp16-activation option only
+  const bool cl = exact_codes(quant_type, lut) && dtype == QZ_DT_F16;
   quant_type &= ~QZ_EXACT_CODES;
 
   if (!vec_ok) {
@@ -1203,7 +1267,7 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   }
 
   int R, WK;
-  choose_geometry(M, K, &R, &WK);
+  choose_geometry(M, K, dtype, &R, &WK);
   set_tables(quant_type, lut, cl, dtype, &p);
   const bool fs = full_steps(K, blocksize, blocksize2, dq, block_base);
   const int rc = cl ? dispatch_tab<true>(p, dtype, dq, fs, R, WK, s) : dispatch_tab<false>(p, dtype, dq, fs, R, WK, s);
@@ -1217,7 +1281,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
   GemvGroup g;
   g.nseg = nseg;
-  const bool cl = exact_codes(quant_type, lut) && dtype != QZ_DT_BF16;
+  const bool cl = exact_codes(quant_type, lut) && dtype == QZ_DT_F16;
   bool all_vec = true;
   long long total_m = 0;
   const bool dq = segs[0].qabsmax != nullptr;
@@ -1242,7 +1306,7 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
     return QZ_OK;
   }
   int R, WK;
-  choose_geometry((int)total_m, K, &R, &WK);
+  choose_geometry((int)total_m, K, dtype, &R, &WK);
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {

@@ -329,6 +329,7 @@ int main(int argc, char **argv) {
   if (bf16) {  // activation dtype: rows per wave for bf16 x (its per-lane convert is shared by R rows)
     GVB(2, QZ_DT_F16, "f16"); GVB(4, QZ_DT_F16, "f16");
     GVB(1, QZ_DT_BF16, "bf16"); GVB(2, QZ_DT_BF16, "bf16"); GVB(4, QZ_DT_BF16, "bf16");
+    GVB(2, QZ_DT_F32, "f32"); GVB(4, QZ_DT_F32, "f32");
   }
   const bool pk = argc > 4 && std::string(argv[4]) == "pack";
   if (pk) {  // y stores: packed row pairs (product) vs one 16-bit store per row (ABL 4096)

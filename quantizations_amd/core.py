@@ -372,6 +372,9 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, blocksi
 # activations -- the reference's numerics -- and fp16 codes for fp16/bf16
 # activations, whose output rounding (2^-11 / 2^-8) is as large as the code
 # rounding.  FP4 is exact either way; a runtime LUT always decodes exactly.
+# Code table of the decode GEMV for fp16 activations: "auto"/"0" = fp16-rounded codes, "1" =
+# exact (hi + lo fp16) codes.  bf16 x always uses bf16 hi + lo codes and fp32 x the fp32
+# codes (the kernel picks the table by activation dtype; the flag is ignored for them).
 GEMV_EXACT_CODES = os.environ.get("QZ_GEMV_EXACT_CODES", "auto")   # "auto" | "1" | "0"
 
 
@@ -385,9 +388,10 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
               state=None, bias: Optional[Tensor] = None, block_base: int = 0,
               exact_codes: Optional[bool] = None) -> Tensor:
     """Batch-1 4-bit GEMV (reference core.py:426-504) as ONE fused kernel:
-    y = x . W^T (+ bias), W from `state`; out dtype = A.dtype.  `exact_codes`
-    (default: GEMV_EXACT_CODES, "auto" = exact for fp32 activations) decodes with
-    the fp32 codebook values."""
+    y = x . W^T (+ bias), W from `state`; out dtype = A.dtype.  fp32 activations are
+    multiplied by the fp32 codebook values and bf16 ones by bf16 hi + lo codes; for fp16
+    activations `exact_codes` (default GEMV_EXACT_CODES) picks the exact hi + lo fp16 codes
+    over the fp16-rounded ones."""
     if state is None:
         raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
     if A.numel() != A.shape[-1]:

@@ -326,7 +326,8 @@ def gemv_parity():
     dequantize_4bit(fp32) is pinned bit-exact to the oracle in tests/).  Each activation
     dtype has its own code table: fp16 x the fp16-rounded codes (default) or the exact
     hi + lo codes; bf16 x bf16 hi + lo codes; fp32 x the fp32 codes.  Outputs are in x's
-    dtype, so the fp16/bf16 figures include the output's own rounding."""
+    dtype, so the fp16/bf16 figures include the output's own rounding (bf16: 2^-9 per
+    element, above the 1e-3 bar by itself; the `_vs_bf16_rounded_ref` figure removes it)."""
     from quantizations_amd.core import dequantize_4bit, gemv_4bit, quantize_4bit
 
     dev = torch.device("cuda")
@@ -345,6 +346,9 @@ def gemv_parity():
             ref = wd @ xx.double()
             y = gemv_4bit(xx.reshape(1, K), packed, state=st, exact_codes=ex).reshape(-1).double()
             row[name] = float(f"{((y - ref).norm() / ref.norm()).item():.3e}")
+            if xdt == torch.bfloat16:  # net of the bf16 output's own rounding (2^-9 per element)
+                rr = ref.to(torch.bfloat16).double()
+                row[name + "_vs_bf16_rounded_ref"] = float(f"{((y - rr).norm() / ref.norm()).item():.3e}")
         res[f"{M}x{K}"] = row
         del wd, packed, st
     from quantizations_amd import _lib, core

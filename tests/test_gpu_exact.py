@@ -185,3 +185,37 @@ def test_bf16_activations_raw_bf16_codes(orc, quant_type, scale):
     ys = gemv_4bit_grouped(xb.to(DEV).reshape(1, K), [(packed, st, None), (packed, st, None)])
     assert torch.equal(ys[0], ys[1])      # (its geometry may split K unlike the single launch)
     assert _rel(ys[0].double().cpu().numpy().ravel(), yref) <= 2.0 ** -8
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("qt", ["nf4", "fp4"])
+def test_runtime_codebook_tables_per_dtype(orc, dt, qt):
+    """qz_gemv_4bit with a runtime codebook (`lut`, the reference ABI's `datatype`) builds the
+    bf16 / fp32 table in kernel: for NF4 it equals the built-in table bit for bit (same codes,
+    same entries); for FP4 the runtime book is the reference LUT (/12 folded into the codes,
+    out_scale 1) against the built-in x12 table, so both are checked against the oracle."""
+    from quantizations_amd import _lib
+    from quantizations_amd.core import quantize_4bit
+
+    M, K = 1024, 4096
+    W = _weights(M, K, seed=41)
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=False)
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=False)
+    x = torch.randn(K, generator=torch.Generator().manual_seed(42)).to(dt).to(DEV)
+    lut = torch.from_numpy(orc.codebook(qt)).to(DEV)
+    am = st.absmax.to(DEV)
+    dcode = _lib.DT_BF16 if dt == torch.bfloat16 else _lib.DT_F32
+    outs = []
+    for use_lut in (False, True):
+        y = torch.empty(M, device=DEV, dtype=dt)
+        rc = _lib.lib.qz_gemv_4bit(M, K, x.data_ptr(), dcode, packed.data_ptr(), _lib.QUANT_TYPES[qt], 64,
+                                   am.data_ptr(), 0, 0, 0, 0, 256, 0, lut.data_ptr() if use_lut else 0, 0,
+                                   y.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        outs.append(y)
+    yref = orc.gemv(x.float().cpu().numpy(), o)
+    tol = 2.0 ** -8 if dt == torch.bfloat16 else EXACT_TOL
+    for y in outs:
+        assert _rel(y.double().cpu().numpy(), yref) <= tol
+    if qt == "nf4":
+        assert torch.equal(outs[0], outs[1])

@@ -34,11 +34,14 @@ extern "C" {
 /* 4-bit codebooks */
 #define QZ_FP4 0 /* bnb FP4 (get_4bit_type("fp4"), core.py:208-229)         */
 #define QZ_NF4 1 /* NF4 codebook q_data (kernels.cu:851)                     */
-/* Flag OR-ed into qz_gemv_4bit(_grouped)'s quant_type: decode with the fp32
- * codes (each split into two fp16 parts, ~2^-23 relative) instead of the
- * fp16-rounded codes of the default byte table.  A runtime `lut` is always
- * decoded this way (the reference GEMV multiplies by its fp32 quant_map,
- * kernels.cu:1115-1120); the built-in FP4 book (x12) is exact either way. */
+/* Flag OR-ed into qz_gemv_4bit(_grouped)'s quant_type for fp16 activations:
+ * decode with the fp32 codes (each split into two fp16 parts, ~2^-23
+ * relative) instead of the fp16-rounded codes of the default byte table.  A
+ * runtime `lut` is always decoded this way; the built-in FP4 book (x12) is
+ * exact either way.  fp32 activations always multiply by the fp32 codes (a
+ * runtime lut verbatim: the reference GEMV's quant_map, kernels.cu:1115-1120)
+ * and bf16 activations by bf16 hi + lo codes (~2^-16); the flag does not
+ * change them. */
 #define QZ_EXACT_CODES 0x100
 
 /* status codes (>0 values are hipError_t) */
@@ -108,8 +111,8 @@ int cdequantize_blockwise_fp32_stream(float *code, unsigned char *A, float *absm
  * r in [0,M), B = packed rows (K/2 bytes each, high nibble first).
  * x/bias/y share `dtype` (QZ_DT_*); accumulation is fp32.  `lut` (16 fp32,
  * device) is optional: NULL selects the built-in codebook of `quant_type`
- * (| QZ_EXACT_CODES: the exact fp32 codes).  fp32/bf16 x of any finite
- * magnitude is taken at fp32-class accuracy (per-chunk power-of-two scaling). */
+ * (| QZ_EXACT_CODES: the exact fp32 codes for fp16 x).  fp32 and bf16 x of
+ * any finite magnitude are multiplied raw (fp32 FMAs / bf16 dot2 into fp32). */
 int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type, int blocksize,
                  const float *absmax, const unsigned char *qabsmax, const float *absmax2, const float *code2,
                  const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,

@@ -116,3 +116,24 @@ def test_gemm16_matches_library_route():
     b = gemm_4bit(X, packed, st, route="blas").double()
     assert ((a - b).norm() / b.norm()).item() < 1e-3
     assert torch.isfinite(a).all()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,K", [(100, 3 * 64), (256, 2112), (1024, 4160), (64, 8192), (4096, 1024)])
+@pytest.mark.parametrize("qt,dq", [("nf4", True), ("fp4", False)])
+def test_gemv_bf16_fp32_tables_on_every_geometry(orc, dt, M, K, qt, dq):
+    """The bf16 / fp32 code tables on every GEMV geometry: K not a multiple of 2048 (the
+    generic step loads), small M (K split over 2-4 waves), ragged K (the scalar kernel), FP4
+    without and NF4 with double quant -- against the oracle's fp32 weight products."""
+    from quantizations_amd.core import gemv_4bit, quantize_4bit
+
+    g = torch.Generator().manual_seed(M + K)
+    W = (torch.randn(M, K, generator=g) * 0.02).half()
+    packed, st = quantize_4bit(W.to(DEV), quant_type=qt, compress_statistics=dq)
+    o = orc.quantize_4bit(W.float().numpy(), 64, qt, double_quant=dq)
+    x = torch.randn(K, generator=g).to(dt)
+    yref = orc.gemv(x.float().numpy(), o)
+    y = gemv_4bit(x.to(DEV).reshape(1, K), packed, state=st).double().cpu().numpy().ravel()
+    tol = 2.0 ** -8 if dt == torch.bfloat16 else 1e-5
+    rel = float(np.linalg.norm(y - yref) / np.linalg.norm(yref))
+    assert rel <= tol, (rel, dt, M, K, qt)

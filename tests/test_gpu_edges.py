@@ -119,7 +119,7 @@ def test_gemm16_matches_library_route():
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,K", [(100, 3 * 64), (256, 2112), (1024, 4160), (64, 8192), (4096, 1024)])
+@pytest.mark.parametrize("M,K", [(100, 3 * 64), (37, 100), (256, 2112), (1024, 4160), (64, 8192), (4096, 1024)])
 @pytest.mark.parametrize("qt,dq", [("nf4", True), ("fp4", False)])
 def test_gemv_bf16_fp32_tables_on_every_geometry(orc, dt, M, K, qt, dq):
     """The bf16 / fp32 code tables on every GEMV geometry: K not a multiple of 2048 (the

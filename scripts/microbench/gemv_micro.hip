@@ -333,7 +333,7 @@ int main(int argc, char **argv) {
   }
   const bool pk = argc > 4 && std::string(argv[4]) == "pack";
   if (pk) {  // y stores: packed row pairs (product) vs one 16-bit store per row (ABL 4096)
-    GVFS(2, 0); GVFS(2, 4096); GVFS(4, 0); GVFS(4, 4096);
+    GVFS(2, 0); GVFS(2, 4096); GVFS(4, 0); GVFS(4, 4096); GVFS(8, 0);
   }
   const bool xcopy = argc > 4 && std::string(argv[4]) == "xcopy";
   if (xcopy) {  // x hot-spot test: every wave reads its own copy of x (ABL 2048)

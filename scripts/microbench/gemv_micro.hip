@@ -331,6 +331,14 @@ int main(int argc, char **argv) {
     GVB(1, QZ_DT_BF16, "bf16"); GVB(2, QZ_DT_BF16, "bf16"); GVB(4, QZ_DT_BF16, "bf16");
     GVB(2, QZ_DT_F32, "f32"); GVB(4, QZ_DT_F32, "f32");
   }
+#define GVK(R, WK) timeit("gemvFS tab dq R=" #R " WK=" #WK, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    const unsigned g = (unsigned)((M + R * (4 / WK) - 1) / (R * (4 / WK))); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, WK, 4, false, 0, true>), dim3(g), dim3(256), 0, 0, q); })
+  const bool wk = argc > 4 && std::string(argv[4]) == "wk";
+  if (wk) {  // K split over waves for long rows (more waves per SIMD when M / R is small)
+    GVK(4, 1); GVK(4, 2); GVK(2, 1); GVK(2, 2); GVK(4, 4);
+  }
   const bool pk = argc > 4 && std::string(argv[4]) == "pack";
   if (pk) {  // y stores: packed row pairs (product) vs one 16-bit store per row (ABL 4096)
     GVFS(2, 0); GVFS(2, 4096); GVFS(4, 0); GVFS(4, 4096); GVFS(8, 0);
@@ -363,7 +371,7 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

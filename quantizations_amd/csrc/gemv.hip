@@ -1106,14 +1106,15 @@ static int ilog2(long long v) {
   return (1LL << l) == v ? l : -1;
 }
 
-// Geometries choose_geometry can return: (R, WK) in {(4,1), (2,1), (1,1), (1,2), (1,4)}.
+// Geometries choose_geometry can return: (R, WK) in {(4,1), (4,2), (2,1), (1,1), (1,2), (1,4)}.
 template <int MODE, bool DQ, int DT, bool FS, bool CL>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
 #define QZ_GV(RR, WW) \
   hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL>), dim3(grid), dim3(256), 0, s, p)
-  if (R == 4) QZ_GV(4, 1);
+  if (R == 4 && WK == 2) QZ_GV(4, 2);
+  else if (R == 4) QZ_GV(4, 1);
   else if (R == 2) QZ_GV(2, 1);
   else if (WK == 1) QZ_GV(1, 1);
   else if (WK == 2) QZ_GV(1, 2);
@@ -1158,6 +1159,10 @@ static void choose_geometry(int M, int K, int dtype, int *R, int *WK) {
   const bool f32 = dtype == QZ_DT_F32;
   *R = (f32 || (long long)M * K >= (1LL << 26)) ? 4 : 2;
   *WK = 1;
+  // * 4 K-steps per row (K = 8192, the Llama-3-70B q/k/v, o and gate/up) at R=4: two waves per
+  //   row, two steps each (profiles/r2_gemv_wk70.txt: 10240x8192 14.0 -> 11.3 us, 8192^2 11.0 ->
+  //   9.4, 57344x8192 55.1 -> 51.5; K = 4096 and 14336 keep WK = 1)
+  if (*R == 4 && nsteps == 4 && !f32) *WK = 2;
   const long long min_waves = f32 ? 1024 : 2048;
   while ((long long)((M + *R - 1) / *R) * (*WK) < min_waves) {
     if (*R > 1) *R >>= 1;
@@ -1327,7 +1332,8 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
   } while (0)
 #define QZ_GR_RW(DQ_, DT_, FS_)                                      \
   do {                                                               \
-    if (R == 4) QZ_GR(DQ_, DT_, 4, 1, FS_);                          \
+    if (R == 4 && WK == 2) QZ_GR(DQ_, DT_, 4, 2, FS_);               \
+    else if (R == 4) QZ_GR(DQ_, DT_, 4, 1, FS_);                     \
     else if (R == 2) QZ_GR(DQ_, DT_, 2, 1, FS_);                     \
     else if (WK == 1) QZ_GR(DQ_, DT_, 1, 1, FS_);                    \
     else if (WK == 2) QZ_GR(DQ_, DT_, 1, 2, FS_);                    \

@@ -632,6 +632,83 @@ def cpu_baseline(runs: int = 20, warmups: int = 3):
                       f"token (extrapolated, not a decode run)"}
 
 
+def decode_layout(args, world: int, sharded: bool):
+    """(weak, tp_mode, global batch).  Strong scaling (default): ONE global batch (bs=1)
+    for any N, every Linear4bit row-split over all N GPUs + all-gather.  --weak: every
+    GPU adds one bs=1 stream (global batch batch x N) and the layers are TP-paired."""
+    weak = args.weak and sharded
+    tp_mode = args.tp_mode or ("pair" if weak else "gather")
+    return weak, tp_mode, (args.batch * world if weak else args.batch)
+
+
+def parallelism_name(tp_mode: str, world: int, sharded: bool) -> str:
+    if not sharded:
+        return "single"
+    return f"tp{world}-megatron-pair-allreduce" if tp_mode == "pair" else f"tp{world}-rowsplit-allgather"
+
+
+def launch_ranks(n: int, port: int = 0) -> int:
+    """Start `n` ranks of this same command line through torch.distributed.run (one
+    process per GPU, rendezvous on 127.0.0.1) and return the launcher's exit status.
+    Called before any GPU work in this process."""
+    import socket
+    import subprocess
+
+    if not port:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this driver
+    log(f"bench: starting {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def selftest_main(args, rank: int, world: int):
+    """CPU rehearsal of the N-rank entry point (tests/test_bench_entry.py): gloo instead
+    of RCCL, the tiny Linear4bit Llama and the shard-local product of the TEST module
+    named by --selftest (the product's local product is the HIP GEMV), and bench's own
+    layout (prepare_decode_model) and decode loop (decode_bench_graph, eager on CPU).
+    Prints the headline line's layout keys plus whether the greedy tokens equal the
+    unsharded reference model's; exits non-zero when they do not."""
+    import importlib
+
+    hook = importlib.import_module(args.selftest)
+    dist.init_process_group("gloo")
+    if dist.get_world_size() != args.gpus:
+        log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+        sys.exit(2)
+    sharded = world > 1 or args.force_shard
+    weak, tp_mode, gbatch = decode_layout(args, world, sharded)
+    cfg, model, ref = hook.tiny_model()
+    n_groups, _ = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
+                                       layer_ops="none", local_matmul=hook.local_matmul)
+    dt, hist = decode_bench_graph(model, cfg, args.steps, args.warmup, args.prompt, world, gbatch,
+                                  graph=False, device="cpu")
+    _, ref_hist = decode_bench_graph(ref, cfg, args.steps, args.warmup, args.prompt, 1, gbatch,
+                                     graph=False, device="cpu")
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    same = torch.tensor([int(torch.equal(hist, ref_hist))])
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"metric": "selftest decode tokens/sec (tiny Llama, CPU, gloo)",
+                          "value": round(args.steps * gbatch / float(t.item()), 3), "unit": "tokens/s",
+                          "n_gpus": dist.get_world_size(), "steps": args.steps, "warmup": args.warmup,
+                          "scaling": "weak" if weak else "strong",
+                          "config": {"workload": "selftest-tiny-llama", "global_batch": gbatch,
+                                     "parallelism": parallelism_name(tp_mode, world, sharded),
+                                     "projection_groups": n_groups},
+                          "selftest": {"tokens_equal_unsharded": bool(same.item())}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if not same.item():
+        sys.exit(3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -673,21 +750,39 @@ def main():
     ap.add_argument("--strong", action="store_true", help="(default) N > 1: the global batch stays --batch")
     ap.add_argument("--no-extra-weak", action="store_true",
                     help="N > 1: skip the extra weak-scaling (TP-pair, global batch N) measurement")
+    ap.add_argument("--selftest", default=None, help=argparse.SUPPRESS)  # CPU test hook module (tests/)
+    ap.add_argument("--master-port", type=int, default=0,
+                    help="rendezvous port when bench.py starts the N ranks itself (0 = a free port)")
     args = ap.parse_args()
     global CAPTURE_MODE
     CAPTURE_MODE = args.capture_mode
     if args.weak and args.strong:
         ap.error("--weak and --strong are exclusive")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here, before
+        # anything touches the GPU, one child process per GPU (torch.distributed.run
+        # sets RANK / LOCAL_RANK / WORLD_SIZE), and exit with the launcher's status.
+        sys.exit(launch_ranks(args.gpus, args.master_port))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a {world}-rank run "
+            f"as {args.gpus} GPUs")
+        sys.exit(2)
+    if args.selftest:
+        return selftest_main(args, rank, world)
     torch.cuda.set_device(local)
     sharded = world > 1 or args.force_shard
     if sharded:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+            sys.exit(2)
 
     if args.gemv_only:
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
@@ -734,16 +829,9 @@ def main():
         return float(t.item()), mode, cfg, n_groups, n_layer_ops
 
     def parallelism(tp_mode: str) -> str:
-        if not sharded:
-            return "single"
-        return f"tp{world}-megatron-pair-allreduce" if tp_mode == "pair" else f"tp{world}-rowsplit-allgather"
+        return parallelism_name(tp_mode, world, sharded)
 
-    # Strong scaling (default): ONE global batch (bs=1) for any N, every Linear4bit
-    # row-split over all N GPUs + all-gather.  --weak: every GPU adds one bs=1
-    # stream (global batch batch x N) and the layers are TP-paired.
-    weak = args.weak and sharded
-    tp_mode = args.tp_mode or ("pair" if weak else "gather")
-    gbatch = args.batch * world if weak else args.batch
+    weak, tp_mode, gbatch = decode_layout(args, world, sharded)
     dt, mode, cfg, n_groups, n_layer_ops = run_decode(tp_mode, gbatch, args.steps, args.warmup)
     tok_s = args.steps * gbatch / dt   # tokens generated by all streams, whole job
 

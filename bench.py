@@ -64,7 +64,8 @@ def log(*a):
 
 
 def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_type: str = "nf4",
-                double_quant: bool = True, dtype: torch.dtype = torch.float16):
+                double_quant: bool = True, dtype: torch.dtype = torch.float16,
+                compute_dtype: torch.dtype = torch.float32):
     from transformers import LlamaConfig, LlamaForCausalLM
 
     from quantizations_amd.integration import replace_with_bnb_linear
@@ -80,7 +81,7 @@ def build_model(layers: int, seed: int, model_name: str = "llama3-8b", quant_typ
     model.eval()
     replace_with_bnb_linear(model, modules_to_not_convert=["lm_head"], quant_type=quant_type,
                             compress_statistics=double_quant,
-                            compute_dtype=torch.float32)
+                            compute_dtype=compute_dtype)
     torch.cuda.empty_cache()
     return model, cfg
 
@@ -225,8 +226,9 @@ def gemv_roofline(copies: int = 64, iters: int = 400):
     fn = _lib.lib.qz_gemv_4bit
 
     from quantizations_amd import core
-    # what Linear4bit launches for fp16 activations
-    prod_qt = core._gemv_quant_type("nf4", None, torch.float16)
+    # what the bench model's Linear4bit (compute_dtype fp32, the reference default) launches
+    # for fp16 activations: the exact codes (core.exact_codes_for)
+    prod_qt = core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32), torch.float16)
     alt_qt = prod_qt ^ _lib.EXACT_CODES
     qt_flags = [prod_qt]
 
@@ -394,22 +396,31 @@ def dominant_roofline(copies: int = 8, iters: int = 100):
     x = torch.randn(1, 1, 4096, device=dev).to(torch.float16)
     outs = [torch.empty(14336, device=dev, dtype=torch.float16) for _ in range(2)]
     sets = [[(p, q, b, 0, o) for (p, q, b), o in zip(items, outs)] for items in sets]
-    for i in range(2 * copies):
-        gemv_4bit_grouped(x, sets[i % copies])
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(100_000_000)
-    e0.record()
-    for i in range(iters):
-        gemv_4bit_grouped(x, sets[i % copies])
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / iters
+    from quantizations_amd.core import exact_codes_for
+
+    def timed(exact):
+        for i in range(2 * copies):
+            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(100_000_000)
+        e0.record()
+        for i in range(iters):
+            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / iters
+
+    prod = exact_codes_for(torch.float32)      # the bench model's Linear4bit (compute_dtype fp32)
+    us = timed(prod)
+    other_us = timed(not prod)
     nbytes = gemv_alg_bytes([(14336, 4096)] * 2)
     return {"kernel": "k_gemv_4bit_grouped gate/up 2 x 14336x4096 NF4+DQ (one launch per layer)",
+            "codes": "exact (fp32 as hi+lo fp16)" if prod else "fp16",
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+            "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "other_codes_launch_us": round(other_us, 3)}
 
 
 @torch.inference_mode()
@@ -632,6 +643,17 @@ def cpu_baseline(runs: int = 20, warmups: int = 3):
                       f"token (extrapolated, not a decode run)"}
 
 
+def codes_desc(args, compute_dtype) -> str:
+    """The decode GEMV's code table for the bench model (core._gemv_quant_type)."""
+    if args.dtype == "bf16":
+        return "codes as bf16 hi+lo"
+    if args.quant == "fp4":
+        return "FP4 codes, exact"
+    from quantizations_amd import _lib, core
+    exact = core._gemv_quant_type("nf4", core.exact_codes_for(compute_dtype), torch.float16) & _lib.EXACT_CODES
+    return "exact NF4 codes (fp32 as hi+lo fp16)" if exact else "fp16-rounded NF4 codes"
+
+
 def decode_layout(args, world: int, sharded: bool):
     """(weak, tp_mode, global batch).  Strong scaling (default): ONE global batch (bs=1)
     for any N, every Linear4bit row-split over all N GPUs + all-gather.  --weak: every
@@ -750,6 +772,11 @@ def main():
     ap.add_argument("--strong", action="store_true", help="(default) N > 1: the global batch stays --batch")
     ap.add_argument("--no-extra-weak", action="store_true",
                     help="N > 1: skip the extra weak-scaling (TP-pair, global batch N) measurement")
+    ap.add_argument("--compute-dtype", choices=("fp32", "fp16"), default="fp32",
+                    help="Linear4bit compute_dtype: fp32 = the reference default (fp16 x decoded against the "
+                         "exact fp32 codes); fp16 = the fp16-rounded code table")
+    ap.add_argument("--no-extra-codes", action="store_true",
+                    help="N = 1: skip the second decode measurement with the other code table")
     ap.add_argument("--selftest", default=None, help=argparse.SUPPRESS)  # CPU test hook module (tests/)
     ap.add_argument("--master-port", type=int, default=0,
                     help="rendezvous port when bench.py starts the N ranks itself (0 = a free port)")
@@ -800,11 +827,14 @@ def main():
 
     layer_ops = "none" if args.no_layer_ops else args.layer_ops
 
-    def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int):
+    compute_dtype = torch.float32 if args.compute_dtype == "fp32" else torch.float16
+
+    def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int, cdt: torch.dtype = compute_dtype):
         t_build = time.perf_counter()
         model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
                                  double_quant=not args.no_dq,
-                                 dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16)
+                                 dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16,
+                                 compute_dtype=cdt)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
                                                      layer_ops=layer_ops)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
@@ -843,6 +873,18 @@ def main():
         extra_weak = {"value": round(w_steps * args.batch * world / wdt, 3), "unit": "tokens/s",
                       "ms_per_step": round(wdt / w_steps * 1e3, 4), "steps": w_steps, "scaling": "weak",
                       "global_batch": args.batch * world, "decode": wmode, "parallelism": parallelism("pair")}
+
+    extra_codes = None
+    if world == 1 and not sharded and not args.no_extra_codes and args.dtype == "fp16" and args.quant == "nf4":
+        # the same decode with the other fp16-activation code table (reported beside the headline)
+        other = torch.float16 if compute_dtype == torch.float32 else torch.float32
+        c_steps = max(16, args.steps // 2)
+        cdt_, cmode, _, _, _ = run_decode(tp_mode, gbatch, c_steps, args.warmup, cdt=other)
+        extra_codes = {"value": round(c_steps * gbatch / cdt_, 3), "unit": "tokens/s",
+                       "ms_per_step": round(cdt_ / c_steps * 1e3, 4), "steps": c_steps, "decode": cmode,
+                       "compute_dtype": "fp32" if other == torch.float32 else "fp16",
+                       "codes": "exact NF4 codes (fp32 as hi+lo fp16)" if other == torch.float32
+                       else "fp16-rounded NF4 codes"}
 
     roof = None
     parity = None
@@ -898,8 +940,8 @@ def main():
             "value": round(tok_s, 3), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak" if weak else "strong", "vs_baseline": None,
-            "dtype": f"{'bf16' if args.dtype == 'bf16' else 'f16'} activations x 4-bit {args.quant.upper()} weights, "
-                     "fp32 accumulate",
+            "dtype": f"{'bf16' if args.dtype == 'bf16' else 'f16'} activations x 4-bit {args.quant.upper()} weights "
+                     f"({codes_desc(args, compute_dtype)}), fp32 accumulate",
             "data": f"synthetic (random-init {'Llama-3-70B' if args.model == 'llama3-70b' else 'Llama-3-8B'} "
                     "architecture, random prompt)",
             "config": {"workload": f"{args.model}-{args.quant}{'' if args.no_dq else '-dq'}"
@@ -911,6 +953,9 @@ def main():
                        "projection_groups": n_groups, "layer_ops": n_layer_ops},
             "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
+        line["config"]["compute_dtype"] = args.compute_dtype
+        if extra_codes is not None:
+            line["decode_other_codes"] = extra_codes
         if layer is not None:
             line["rowsplit_layer"] = layer
         if extra_weak is not None:

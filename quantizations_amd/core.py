@@ -362,19 +362,17 @@ def dequantize_4bit(A: Tensor, quant_state: Optional[QuantState] = None, blocksi
     return out.t()
 
 
-# Decode GEMV codebook precision.  The reference's only exported GEMV takes fp32
-# activations and multiplies by its fp32 quant_map (kernels.cu:1115-1120); bnb's
-# fp16 GEMV holds the codebook in the activation type.  The byte-table decode
-# either holds the codes as fp16 (<= 2.4e-4 relative per NF4 code) or, with exact
-# codes, splits each fp32 code into two fp16 parts (~2^-23: fp32-class) at the cost
-# of one more dot product per weight pair (+3 % at 4096^2, +13 % on the grouped
-# gate/up launch).  "auto" (default): exact codes for fp32
-# activations -- the reference's numerics -- and fp16 codes for fp16/bf16
-# activations, whose output rounding (2^-11 / 2^-8) is as large as the code
-# rounding.  FP4 is exact either way; a runtime LUT always decodes exactly.
-# Code table of the decode GEMV for fp16 activations: "auto"/"0" = fp16-rounded codes, "1" =
-# exact (hi + lo fp16) codes.  bf16 x always uses bf16 hi + lo codes and fp32 x the fp32
-# codes (the kernel picks the table by activation dtype; the flag is ignored for them).
+# Decode GEMV code table, chosen by activation dtype (the kernel picks the table; see
+# _gemv_quant_type and gemv.hip's qz_gemv_4bit):
+#  * fp32 x: the fp32 codebook values multiplied into the raw x (v_fma_f32) -- the
+#    reference's own numerics (kernels.cu:1115-1120,1169-1170); the flag is ignored.
+#  * bf16 x: each code as bf16 hi + lo (~2^-16) dotted against the raw bf16 x pairs;
+#    the flag is ignored.
+#  * fp16 x: `exact_codes` picks the exact codes (c * 2^14 = hi + lo fp16 parts, fp32-class)
+#    over the fp16-rounded codes (<= 2.4e-4 relative per NF4 code).  Linear4bit passes
+#    exact_codes=True when its compute_dtype is fp32 (the reference default: the layer's
+#    products are then the reference's), otherwise None = this default: "auto"/"0" =
+#    fp16-rounded codes, "1" = exact codes.  FP4 codes are exact in either table.
 GEMV_EXACT_CODES = os.environ.get("QZ_GEMV_EXACT_CODES", "auto")   # "auto" | "1" | "0"
 
 
@@ -382,6 +380,16 @@ def _gemv_quant_type(quant_type: str, exact_codes: Optional[bool], dtype: torch.
     if exact_codes is None:
         exact_codes = dtype == torch.float32 if GEMV_EXACT_CODES == "auto" else GEMV_EXACT_CODES == "1"
     return _lib.QUANT_TYPES[quant_type] | (_lib.EXACT_CODES if exact_codes else 0)
+
+
+def exact_codes_for(compute_dtype):
+    """Decode code table for a layer's compute_dtype.  The reference casts x to
+    compute_dtype (modules.py:141-142); with fp32 -- its config default -- the GEMV
+    multiplies x by the fp32 codebook values (kernels.cu:1115-1120,1169-1170).  An
+    fp16 x is exact in fp32, so skipping the cast and dotting the fp16 x against the
+    exact (hi + lo) codes gives the reference's products; other compute dtypes keep
+    the default table (GEMV_EXACT_CODES)."""
+    return True if compute_dtype == torch.float32 else None
 
 
 def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
@@ -467,18 +475,23 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
 # fused_max_tokens(M) tokens and the dequant route above it (DESIGN.md
 # section 4.2 has the measured crossovers: hipBLASLt is 12-17 % faster than
 # qz_gemm_16bit at T >= 4096 today, so it stays the default).
-PREFILL_FUSED_MAX_TOKENS = int(os.environ.get("QZ_PREFILL_FUSED_MAX_T", "512"))
+_FUSED_MAX_T_ENV = os.environ.get("QZ_PREFILL_FUSED_MAX_T")
+PREFILL_FUSED_MAX_TOKENS = int(_FUSED_MAX_T_ENV) if _FUSED_MAX_T_ENV else None   # None = the measured table
 PREFILL_GEMM16 = os.environ.get("QZ_PREFILL_GEMM16", "0") == "1"
 GEMM16_MIN_TILES = int(os.environ.get("QZ_GEMM16_MIN_TILES", "256"))
 
 
-def fused_max_tokens(M: int) -> int:
-    """Largest token count the auto route sends to the fused kernels for an M-row
-    weight: the measured crossover against dequantize_4bit + hipBLASLt, whole routes
-    (scripts/prefill_lowT_sweep.py, profiles/r2_prefill_lowT_sweep.txt; Llama-3-8B
-    shapes): 256 tokens for 2048..8192 rows (4096x4096, 4096x14336), 128 otherwise
-    (1024x4096, 14336x4096); never above PREFILL_FUSED_MAX_TOKENS."""
-    return min(PREFILL_FUSED_MAX_TOKENS, 256 if 2048 <= M <= 8192 else 128)
+def fused_max_tokens(M: int, K: int = 4096) -> int:
+    """Largest token count the auto route sends to the fused kernels for an M x K
+    weight.  An explicit QZ_PREFILL_FUSED_MAX_T (PREFILL_FUSED_MAX_TOKENS) replaces the
+    table.  The table is the measured crossover against dequantize_4bit + hipBLASLt,
+    whole routes (scripts/prefill_lowT_sweep.py, profiles/r2_prefill_lowT_sweep.txt),
+    measured on the Llama-3-8B shapes only (K = 4096 / 14336): 256 tokens for
+    2048..8192 rows, 128 otherwise.  Other K (the 70B shapes, K = 8192 / 28672) take
+    the same rows rule, unmeasured."""
+    if PREFILL_FUSED_MAX_TOKENS is not None:
+        return PREFILL_FUSED_MAX_TOKENS
+    return 256 if 2048 <= M <= 8192 else 128
 
 
 def gemm_16bit(A: Tensor, W: Tensor, bias: Optional[Tensor] = None) -> Optional[Tensor]:
@@ -533,7 +546,7 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
     if route == "fused" and not fused_ok:
         raise ValueError("gemm_4bit: the fused kernel needs fp16/bf16 activations, K % 64 == 0, M % 4 == 0 "
                          "and blocksize >= 64")
-    if fused_ok and (route == "fused" or (route == "auto" and T <= fused_max_tokens(M))):
+    if fused_ok and (route == "fused" or (route == "auto" and T <= fused_max_tokens(M, K))):
         out = torch.empty((T, M), dtype=A.dtype, device=A.device)
         if bias is not None and bias.dtype != A.dtype:
             bias = bias.to(A.dtype)
@@ -550,6 +563,9 @@ def gemm_4bit(A: Tensor, B: Tensor, state: QuantState, bias: Optional[Tensor] = 
         Y = gemm_16bit(A, W, bias)
         if Y is not None:
             return Y
+    if route == "gemm16":  # asked for our GEMM explicitly: never a silent library fallback
+        raise ValueError("gemm_4bit: route 'gemm16' needs fp16/bf16 activations, K % 64 == 0, M % 8 == 0 and "
+                         "16-byte aligned operands")
     return torch.nn.functional.linear(A, W.to(A.dtype), None if bias is None else bias.to(A.dtype))
 
 

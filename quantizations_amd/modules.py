@@ -14,16 +14,18 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .core import (MT_MAX_TOKENS, Params4bit, QuantState, dequantize_4bit, gemm_4bit, gemm_4bit_grouped, gemv_4bit,
-                   gemv_4bit_grouped, grouped_tokens_ok)
+from .core import (MT_MAX_TOKENS, Params4bit, QuantState, dequantize_4bit, exact_codes_for, gemm_4bit,
+                   gemm_4bit_grouped, gemv_4bit, gemv_4bit_grouped, grouped_tokens_ok)
 
 
-def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None):
+def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None,
+                exact_codes=None):
     """x . W^T (+ bias) for a 4-bit W (reference modules.py:28-64).  `B` is the packed
-    weight (the reference passes ``weight.t()``; only its storage is used)."""
+    weight (the reference passes ``weight.t()``; only its storage is used).
+    `exact_codes` (decode only): see gemv_4bit; Linear4bit sets it from compute_dtype."""
     assert quant_state is not None
     if A.numel() == A.shape[-1]:
-        return gemv_4bit(A, B, out, state=quant_state, bias=bias)
+        return gemv_4bit(A, B, out, state=quant_state, bias=bias, exact_codes=exact_codes)
     return gemm_4bit(A, B, quant_state, bias=bias)
 
 
@@ -79,11 +81,12 @@ def _linear4bit_group_compute(group: DecodeGroup, x: torch.Tensor):
         bias = None if m.bias is None else m.bias.to(xin.dtype)
         items.append((m.weight, m.weight.quant_state, bias))
     if xin.numel() == xin.shape[-1]:
-        outs = gemv_4bit_grouped(xin, items)
+        outs = gemv_4bit_grouped(xin, items, exact_codes=exact_codes_for(m0.compute_dtype))
     elif grouped_tokens_ok(xin, items):
         outs = gemm_4bit_grouped(xin, items)
     else:  # shapes the multi-token kernel does not take: each member as it would run alone
-        outs = [matmul_4bit(xin, w, bias=b, quant_state=st) for w, st, b in items]
+        outs = [matmul_4bit(xin, w, bias=b, quant_state=st, exact_codes=exact_codes_for(m0.compute_dtype))
+                for w, st, b in items]
     return [o if o.dtype == inp_dtype else o.to(inp_dtype) for o in outs]
 
 
@@ -130,7 +133,8 @@ class Linear4bit(nn.Linear):
         inp_dtype = x.dtype
         xin = self._input(x)
         bias = None if self.bias is None else self.bias.to(xin.dtype)
-        out = matmul_4bit(xin, self.weight, bias=bias, quant_state=qs)
+        out = matmul_4bit(xin, self.weight, bias=bias, quant_state=qs,
+                          exact_codes=exact_codes_for(self.compute_dtype))
         return out if out.dtype == inp_dtype else out.to(inp_dtype)
 
     # -- checkpoints: bnb-compatible keys (QuantState.as_dict(packed=True)) --

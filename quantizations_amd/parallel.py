@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .core import QuantState
+from .core import QuantState, exact_codes_for
 
 
 @dataclass
@@ -95,13 +95,15 @@ class RowShardedLinear4bit(nn.Module):
         bias = None if full.bias is None else full.bias.data[shard.r0:shard.r1].clone()
         self.register_buffer("bias", bias, persistent=False)
         self._local_matmul = local_matmul  # test hook; None = the fused HIP kernels
+        self.exact_codes = exact_codes_for(getattr(full, "compute_dtype", None))
 
     def local_forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._local_matmul is not None:
             return self._local_matmul(x, self)
         from .core import gemm_4bit, gemv_4bit
         if x.numel() == x.shape[-1]:
-            return gemv_4bit(x, self.packed, state=self.state, bias=self.bias, block_base=self.block_base)
+            return gemv_4bit(x, self.packed, state=self.state, bias=self.bias, block_base=self.block_base,
+                             exact_codes=self.exact_codes)
         if self.block_base != 0:
             raise ValueError("prefill on a shard needs block-aligned second-level scales")
         return gemm_4bit(x, self.packed, self.state, bias=self.bias)
@@ -180,7 +182,8 @@ def sharded_group_compute(group, x: torch.Tensor):
         for m, v in zip(ms, views):
             v.copy_(m._local_matmul(x, m).reshape(-1))
     else:
-        gemv_4bit_grouped(x, [(m.packed, m.state, m.bias, m.block_base, v) for m, v in zip(ms, views)])
+        gemv_4bit_grouped(x, [(m.packed, m.state, m.bias, m.block_base, v) for m, v in zip(ms, views)],
+                          exact_codes=ms[0].exact_codes)
     lead = x.shape[:-1]
     if not ms[0].gather:  # column-parallel: each member keeps its shard
         return [v.view(*lead, r) for v, r in zip(views, rows)]
@@ -260,6 +263,7 @@ class RowParallelLinear4bit(nn.Module):
         bias = None if (full.bias is None or self.rank != 0) else full.bias.data.clone()
         self.register_buffer("bias", bias, persistent=False)
         self._local_matmul = local_matmul  # test hook; None = the fused HIP kernels
+        self.exact_codes = exact_codes_for(getattr(full, "compute_dtype", None))
 
     def forward(self, x_local: torch.Tensor) -> torch.Tensor:
         if x_local.shape[-1] != self.k1 - self.k0:
@@ -270,7 +274,7 @@ class RowParallelLinear4bit(nn.Module):
         else:
             from .core import gemm_4bit, gemv_4bit
             if x_local.numel() == x_local.shape[-1]:
-                y = gemv_4bit(x_local, self.packed, state=self.state, bias=self.bias)
+                y = gemv_4bit(x_local, self.packed, state=self.state, bias=self.bias, exact_codes=self.exact_codes)
             else:
                 y = gemm_4bit(x_local, self.packed, self.state, bias=self.bias)
         y32 = y.float().contiguous()   # [..., M] fp32: 16 KiB at bs=1 for M = 4096

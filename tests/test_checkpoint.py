@@ -160,8 +160,9 @@ def test_oracle_built_checkpoint_loaded_on_gpu_matches_oracle(tmp_path, orc, qt)
     """A safetensors file written from ORACLE-built quant states (packed bytes,
     qabsmax, absmax2, offset under the core.py:29-42 keys) -- no GPU kernel
     produced any of it -- loaded with load_quantized onto the GPU: Linear4bit
-    decode (the fused GEMV, exact codes and default table), prefill, and
-    gemv_4bit on the loaded state all match oracle.gemv of the same bytes."""
+    decode (the fused GEMV, default fp16 table), gemv_4bit on the loaded state with fp32 x
+    (fp32 codes) and with fp16 x + exact codes, and prefill all match oracle.gemv of the
+    same bytes."""
     from safetensors.torch import save_file
 
     from quantizations_amd.core import gemv_4bit
@@ -194,9 +195,15 @@ def test_oracle_built_checkpoint_loaded_on_gpu_matches_oracle(tmp_path, orc, qt)
         y = lin(x.cuda()).float().cpu().numpy().ravel()
         rel = np.linalg.norm(y - yref) / np.linalg.norm(yref)
         assert rel <= 1e-3, (name, rel)
-        ye = gemv_4bit(x.float().cuda(), lin.weight, state=lin.weight.quant_state, exact_codes=True)
+        # fp32 x: the fp32 code table, fp32 output
+        ye = gemv_4bit(x.float().cuda(), lin.weight, state=lin.weight.quant_state)
         rel_e = np.linalg.norm(ye.cpu().numpy().ravel() - yref) / np.linalg.norm(yref)
         assert rel_e <= 1e-5, (name, rel_e)
+        # fp16 x with exact_codes=True (the exact hi + lo fp16 table): the reference value
+        # rounded once to the fp16 output, plus fp32 summation noise
+        yh = gemv_4bit(x.cuda(), lin.weight, state=lin.weight.quant_state, exact_codes=True)
+        yh = yh.double().cpu().numpy().ravel()
+        assert np.all(np.abs(yh - yref) <= 2.0 ** -11 * np.abs(yref) + 1e-5 * np.max(np.abs(yref))), name
         X = torch.randn(3, 7, K, generator=torch.Generator().manual_seed(K)).half()
         Yref = X.reshape(-1, K).double().numpy() @ orc.dequantize(o).astype(np.float16).astype(np.float64).T
         Y = lin(X.cuda()).double().cpu().numpy().reshape(-1, M)

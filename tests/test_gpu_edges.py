@@ -105,6 +105,30 @@ def test_gemm16_route_vs_fp64(T, M, dtype):
     assert worst <= 0, f"elementwise bound exceeded by {worst:.3e}"
 
 
+@pytest.mark.parametrize("T,M,K", [(37, 264, 64), (300, 520, 128), (257, 1032, 192), (1, 8, 64)])
+def test_gemm16_short_k_loops(T, M, K):
+    """qz_gemm_16bit with 1-, 2- and 3-step K loops (K = 64 / 128 / 192; the prologue and the
+    last steps of the 8-phase schedule) and ragged T / M."""
+    y, ref = _gemm16_case(T, M, K, torch.float16, bias=True, seed=T * M + K)
+    assert y.shape == (T, M)
+    worst = ((y.double() - ref).abs() - (1e-3 * ref.abs().max() + 2.0 ** -10 * ref.abs())).max().item()
+    assert worst <= 0, f"elementwise bound exceeded by {worst:.3e}"
+
+
+def test_gemm16_route_rejects_unsupported_shape():
+    """route='gemm16' raises where qz_gemm_16bit does not apply (M % 8 != 0) instead of
+    silently running the library GEMM; route='auto' takes the library GEMM there."""
+    from quantizations_amd.core import gemm_4bit, quantize_4bit
+
+    W = (torch.randn(1028, 256, device=DEV) * 0.02).half()
+    packed, st = quantize_4bit(W, quant_type="nf4")
+    X = torch.randn(300, 256, device=DEV).half()
+    with pytest.raises(ValueError):
+        gemm_4bit(X, packed, st, route="gemm16")
+    y = gemm_4bit(X, packed, st, route="auto")
+    assert y.shape == (300, 1028) and torch.isfinite(y).all()
+
+
 def test_gemm16_matches_library_route():
     """The two dequant routes multiply the same operand: gemm16 vs the library GEMM."""
     from quantizations_amd.core import gemm_4bit, quantize_4bit
@@ -119,13 +143,15 @@ def test_gemm16_matches_library_route():
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,K", [(100, 3 * 64), (37, 100), (256, 2112), (1024, 4160), (64, 8192), (4096, 1024)])
+@pytest.mark.parametrize("M,K", [(100, 3 * 64), (37, 100), (256, 2112), (1024, 4160), (64, 8192), (4096, 1024),
+                                 (8192, 8192), (28672, 8192)])
 @pytest.mark.parametrize("qt,dq", [("nf4", True), ("fp4", False)])
 def test_gemv_bf16_fp32_tables_on_every_geometry(orc, dt, M, K, qt, dq):
     """The bf16 / fp32 code tables on every GEMV geometry: K not a multiple of 2048 (the
-    generic step loads), small M (K split over 2-4 waves), ragged K (the scalar kernel), FP4
-    without and NF4 with double quant -- against the oracle's fp32 weight products."""
-    from quantizations_amd.core import gemv_4bit, quantize_4bit
+    generic step loads), small M (K split over 2-4 waves), ragged K (the scalar kernel), the
+    Llama-3-70B rows of 8192 (R = 4, WK = 2), FP4 without and NF4 with double quant, single
+    and grouped launches -- against the oracle's fp32 weight products."""
+    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, quantize_4bit
 
     g = torch.Generator().manual_seed(M + K)
     W = (torch.randn(M, K, generator=g) * 0.02).half()
@@ -134,6 +160,9 @@ def test_gemv_bf16_fp32_tables_on_every_geometry(orc, dt, M, K, qt, dq):
     x = torch.randn(K, generator=g).to(dt)
     yref = orc.gemv(x.float().numpy(), o)
     y = gemv_4bit(x.to(DEV).reshape(1, K), packed, state=st).double().cpu().numpy().ravel()
+    # the grouped launch (the R = 4, WK = 2 K-split geometry at K = 8192) returns the same outputs
+    (yg,) = gemv_4bit_grouped(x.to(DEV).reshape(1, K), [(packed, st, None)])
+    assert np.array_equal(yg.double().cpu().numpy().ravel(), y)
     tol = 2.0 ** -8 if dt == torch.bfloat16 else 1e-5
     rel = float(np.linalg.norm(y - yref) / np.linalg.norm(yref))
     assert rel <= tol, (rel, dt, M, K, qt)

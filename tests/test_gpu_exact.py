@@ -62,7 +62,8 @@ def test_reference_abi_gemv_exact_codes(orc, qt, shape):
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("shape", [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)])
+@pytest.mark.parametrize("shape", [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336), (8192, 8192),
+                                   (28672, 8192)])
 def test_gemv_exact_nf4_codes(orc, dt, shape):
     """Built-in NF4 with exact_codes=True (QZ_EXACT_CODES), single and grouped
     launches, double quant: fp32 output within 1e-5; fp16/bf16 outputs are the
@@ -219,3 +220,43 @@ def test_runtime_codebook_tables_per_dtype(orc, dt, qt):
         assert _rel(y.double().cpu().numpy(), yref) <= tol
     if qt == "nf4":
         assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("shape", [(4096, 4096), (14336, 4096), (1024, 8192), (8192, 8192)])
+@pytest.mark.parametrize("compute_dtype", [torch.float32, None])
+def test_linear4bit_decode_honours_compute_dtype(orc, shape, compute_dtype):
+    """Linear4bit(compute_dtype=fp32) -- the reference's config default -- decodes an fp16 x
+    with the reference's fp32 code values (modules.py:141-142 cast x to fp32; kernels.cu:
+    1115-1120,1169-1170): the fp16 output is the oracle's fp32 result rounded once, i.e.
+    |y - yref| <= 2^-11 |yref| (RNE) + 1e-5 max|yref| (fp32 summation order), and at most
+    1 % of the outputs differ from fp16(yref) (values within fp32 noise of a rounding
+    midpoint).  Single layer and the grouped (q/k/v-style) launch.  compute_dtype=None keeps
+    the fp16-rounded table (bounded by 1e-3; its mismatch count is reported)."""
+    import quantizations_amd as qa
+    from quantizations_amd.integration import fuse_projection_groups
+
+    M, K = shape
+    W = _weights(M, K, seed=M + K + 17)
+    o = orc.quantize_4bit(W.float().numpy(), 64, "nf4")
+    parent = torch.nn.Module()
+    for nm in ("q_proj", "k_proj"):
+        m = qa.Linear4bit(K, M, bias=False, compute_dtype=compute_dtype, quant_type="nf4")
+        m.weight = qa.Params4bit(W.clone(), requires_grad=False, quant_type="nf4", module=m)
+        parent.add_module(nm, m.to(DEV))
+    x = torch.randn(1, 1, K, generator=torch.Generator().manual_seed(M ^ K)).half()
+    yref = orc.gemv(x.float().numpy().ravel(), o)
+    y_single = parent.q_proj(x.to(DEV)).reshape(-1)
+    assert fuse_projection_groups(parent, groups=(("q_proj", "k_proj"),)) == 1
+    xd = x.to(DEV)
+    y_group = [parent.q_proj(xd).reshape(-1), parent.k_proj(xd).reshape(-1)]
+    for y in (y_single, *y_group):
+        yc = y.float().cpu().numpy().astype(np.float64)
+        err = np.abs(yc - yref)
+        mism = int(np.sum(yc != yref.astype(np.float16).astype(np.float64)))
+        if compute_dtype is torch.float32:
+            bound = 2.0 ** -11 * np.abs(yref) + EXACT_TOL * np.max(np.abs(yref))
+            assert np.all(err <= bound), float(np.max(err - bound))
+            assert mism <= 0.01 * M, mism
+        else:
+            assert _rel(yc, yref) <= 1e-3
+            print(f"{M}x{K} fp16 codes: {mism} of {M} outputs differ from fp16(yref)")

@@ -172,4 +172,13 @@ def test_fused_route_threshold_follows_measured_crossover():
     assert core.fused_max_tokens(4096) == 256        # 4096x4096, 4096x14336: fused wins to T = 256
     assert core.fused_max_tokens(1024) == 128        # k/v projections: to T = 128
     assert core.fused_max_tokens(14336) == 128       # gate/up: a tie at T = 128, dequant route above
-    assert all(core.fused_max_tokens(m) <= core.PREFILL_FUSED_MAX_TOKENS for m in (8, 4096, 1 << 20))
+    assert core.PREFILL_FUSED_MAX_TOKENS is None     # no QZ_PREFILL_FUSED_MAX_T in the test env
+
+
+def test_fused_route_threshold_env_override_replaces_table(monkeypatch):
+    """An explicit QZ_PREFILL_FUSED_MAX_T replaces the measured table (in both directions)."""
+    from quantizations_amd import core
+
+    for v in (512, 64, 0):
+        monkeypatch.setattr(core, "PREFILL_FUSED_MAX_TOKENS", v)
+        assert all(core.fused_max_tokens(m, k) == v for m in (8, 1024, 4096, 14336) for k in (4096, 8192))

@@ -321,6 +321,69 @@ GEMV_EXTRA = {}
 
 
 @torch.inference_mode()
+def gemv_in_kernel(exact: bool, copies: int = 64, samples: int = 12, burst: int = 30):
+    """In-kernel duration of the 4096x4096 NF4+DQ product GEMV: the same instantiation with
+    s_memrealtime stamps (libqz_diag.so, measurement-only): first wave's start to last
+    wave's end of one launch, the last of `burst` back-to-back launches on a parked stream,
+    median over `samples`.  None when the diagnostic library is absent."""
+    import ctypes
+
+    from quantizations_amd.core import quantize_4bit
+
+    path = os.path.join(REPO, "quantizations_amd", "libqz_diag.so")
+    if not os.path.exists(path):
+        return None
+    diag = ctypes.CDLL(path)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    diag.qz_diag_set_stamp_buffer.argtypes = [vp]
+    diag.qz_diag_gemv_stamped.argtypes = [i32, i32, vp, vp, i32, vp, vp, vp, vp, vp, ctypes.POINTER(i32), vp]
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    W = (torch.randn(4096, 4096, device=dev) * 0.02).to(torch.float16)
+    packed, qs = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+    sets = [(packed.clone(), qs.absmax.clone(), qs.state2.absmax.clone()) for _ in range(copies)]
+    x = torch.randn(4096, device=dev).to(torch.float16)
+    y = torch.empty(4096, device=dev, dtype=torch.float16)
+    stamps = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)   # up to 4096 waves x 8 u64
+    if diag.qz_diag_set_stamp_buffer(stamps.data_ptr()):
+        raise RuntimeError("qz_diag_set_stamp_buffer failed")
+    stream = torch.cuda.current_stream().cuda_stream
+    nw = i32(0)
+
+    def launch(i):
+        p, qa, a2 = sets[i % copies]
+        rc = diag.qz_diag_gemv_stamped(4096, 4096, x.data_ptr(), p.data_ptr(), int(exact), qa.data_ptr(),
+                                       a2.data_ptr(), qs.state2.code.data_ptr(), qs.offset.data_ptr(),
+                                       y.data_ptr(), ctypes.byref(nw), stream)
+        if rc:
+            raise RuntimeError(f"qz_diag_gemv_stamped rc={rc}")
+
+    for i in range(2 * copies):
+        launch(i)
+    torch.cuda.synchronize()
+    spans = []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b2b = []
+    for smp in range(samples):
+        torch.cuda._sleep(20_000_000)
+        e0.record()
+        for i in range(burst):
+            launch(smp * burst + i)
+        e1.record()
+        torch.cuda.synchronize()
+        b2b.append(e0.elapsed_time(e1) * 1e3 / burst)
+        st = stamps.view(-1, 8)[:nw.value].cpu()
+        t0 = int(st[:, 0].min())
+        spans.append((int(st[:, 4].max()) - t0) * 0.01)          # 100 MHz ticks -> us
+    return {"in_kernel_us": round(statistics.median(spans), 3),
+            "in_kernel_us_min": round(min(spans), 3), "in_kernel_us_max": round(max(spans), 3),
+            "stamped_launch_us_avg": round(statistics.median(b2b), 3), "waves": nw.value,
+            "method": "s_memrealtime (100 MHz) at each wave's start and after its stores; max end - min start of "
+                      f"one launch (the last of {burst} back-to-back), median of {samples}; stamped build of the "
+                      "product instantiation (libqz_diag.so)"}
+
+
+@torch.inference_mode()
 def gemv_parity():
     """Decode-GEMV accuracy at the Llama-3-8B shapes (NF4 + double quant): rel err
     ||y - y_ref|| / ||y_ref|| with y_ref the fp64 product of the same x with the fp32
@@ -420,7 +483,17 @@ def dominant_roofline(copies: int = 8, iters: int = 100):
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-            "other_codes_launch_us": round(other_us, 3)}
+            "other_codes_launch_us": round(other_us, 3), "traffic": _pmc_traffic("r3_gateup_pmc.json"),
+            "profile": "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes)"}
+
+
+def _pmc_traffic(name: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary under profiles/."""
+    path = os.path.join(REPO, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
 
 
 @torch.inference_mode()
@@ -749,6 +822,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--gemv-only", action="store_true", help="only the 4096x4096 roofline microbench (profiling)")
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
+    ap.add_argument("--dominant-only", action="store_true",
+                    help="only the grouped gate/up GEMV measurement (the decode step's longest launch; profiling)")
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--no-layer-ops", action="store_true",
@@ -818,6 +893,9 @@ def main():
                           "achieved_GBs": GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9}), flush=True)
         return
 
+    if args.dominant_only:
+        print(json.dumps(dominant_roofline()), flush=True)
+        return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
         return
@@ -894,11 +972,7 @@ def main():
         # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
         # overhead on ROCm and disagrees with rocprofv3, so it is reported only.
         ach = GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9
-        traffic = None
-        pmc = os.path.join(REPO, "profiles", "gemv_4096_pmc.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        traffic = _pmc_traffic("gemv_4096_pmc.json")
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_gemv_4bit<Tab,DQ,f16,R=2,WK=1,full-step,CL=%d> 4096x4096 NF4+DQ (LDS byte-table decode, "
@@ -916,6 +990,14 @@ def main():
                                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline()}
+        from quantizations_amd import _lib, core
+        ink = gemv_in_kernel(bool(core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32), torch.float16)
+                                  & _lib.EXACT_CODES))
+        if ink is not None:
+            # the kernel's own duration (stamps): what the launch period adds on top is dispatch
+            roof["in_kernel"] = ink
+            roof["in_kernel_us"] = ink["in_kernel_us"]
+            roof["frac_in_kernel"] = round(GEMV_BYTES_4096 / (ink["in_kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         parity = gemv_parity()
 
     layer = None

@@ -371,7 +371,20 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk) {
+  const bool stream = argc > 4 && std::string(argv[4]) == "stream";
+#define GVST(R, G, CL_) timeit("stream2 R=" #R " wgs=" #G " CL=" #CL_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    if (CL_) q.out_scale = 1.0f / 16384; q.tabsel = 0; \
+    const int nunits = (M + R - 1) / R; const int g = std::min((int)(G), (nunits + 3) / 4); \
+    hipLaunchKernelGGL((k_gemv_4bit_stream2<true, R, CL_>), dim3(g), dim3(256), 0, 0, q, nunits); })
+  if (stream) {  // persistent streaming form (K = 4096 rows) vs the production full-step kernel
+    GVFS(2, 0); GVFS(4, 0); GVC(4, 0, true);
+    GVST(4, 1024, false); GVST(4, 768, false); GVST(4, 512, false); GVST(4, 896, false);
+    GVST(2, 1024, false); GVST(2, 768, false); GVST(2, 512, false);
+    GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
+    GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
+  }
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

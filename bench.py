@@ -177,7 +177,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 
 
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
-                         fuse: bool = True, layer_ops: str = "all", local_matmul=None):
+                         fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -189,7 +189,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
             apply_tensor_parallel(model, rank, world, local_matmul=local_matmul)
         else:
             from quantizations_amd.parallel import shard_model_linear4bit
-            shard_model_linear4bit(model, rank, world, local_matmul=local_matmul)
+            shard_model_linear4bit(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
         import gc
         gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
         if torch.cuda.is_available():
@@ -498,7 +498,7 @@ def _pmc_traffic(name: str):
 
 @torch.inference_mode()
 def rowsplit_layer(rank: int, world: int, sharded: bool, M: int = 8192, K: int = 28672, calls: int = 20,
-                   reps: int = 5):
+                   reps: int = 5, gatherer=None):
     """one Llama-3-70B-shaped Linear4bit (M x K NF4+DQ, bs = 1) row-split over
     the job's ranks -- each rank's GEMV on M/P rows (slices of the ONE global quant state)
     + the RCCL all-gather of the fp16 shards -- vs the same layer's unsharded GEMV on one
@@ -550,6 +550,12 @@ def rowsplit_layer(rank: int, world: int, sharded: bool, M: int = 8192, K: int =
             out["rows_per_rank"] = shard.r1 - shard.r0
             out["local_gemv_us"] = timed(lambda: shard.local_forward(x))
             out["rowsplit_allgather_us"] = timed(lambda: shard(x))
+            if gatherer is not None:   # the same layer through the one-shot exchange
+                shard.gatherer = gatherer
+                out["rowsplit_oneshot_us"] = timed(lambda: shard(x))
+                got1 = shard(x).reshape(-1)
+                shard.gatherer = None
+                out["oneshot_equals_rccl"] = bool(torch.equal(got1, shard(x).reshape(-1)))
             ref, got = full(x).reshape(-1), shard(x).reshape(-1)
             # same products; a shard's GEMV may split K differently (fp32 summation order)
             out["bit_identical_to_unsharded"] = bool(torch.equal(got, ref))
@@ -742,6 +748,21 @@ def parallelism_name(tp_mode: str, world: int, sharded: bool) -> str:
     return f"tp{world}-megatron-pair-allreduce" if tp_mode == "pair" else f"tp{world}-rowsplit-allgather"
 
 
+def setup_oneshot(rank: int):
+    """The one-shot IPC all-gather for the row-split layers, verified against RCCL on live
+    data; (None, "rccl (...)") when it cannot be set up or disagrees."""
+    try:
+        from quantizations_amd.exchange import OneShotAllGather
+        g = OneShotAllGather(slot_bytes=1 << 18)
+        if g.verify():
+            return g, "oneshot-ipc"
+        log(f"[rank {rank}] one-shot all-gather disagrees with RCCL: using RCCL")
+        return None, "rccl (one-shot failed verification)"
+    except Exception as e:  # reported in the line, never fatal to the measurement
+        log(f"[rank {rank}] one-shot all-gather unavailable ({type(e).__name__}: {e}): using RCCL")
+        return None, f"rccl (one-shot unavailable: {type(e).__name__})"
+
+
 def launch_ranks(n: int, port: int = 0) -> int:
     """Start `n` ranks of this same command line through torch.distributed.run (one
     process per GPU, rendezvous on 127.0.0.1) and return the launcher's exit status.
@@ -847,6 +868,9 @@ def main():
     ap.add_argument("--strong", action="store_true", help="(default) N > 1: the global batch stays --batch")
     ap.add_argument("--no-extra-weak", action="store_true",
                     help="N > 1: skip the extra weak-scaling (TP-pair, global batch N) measurement")
+    ap.add_argument("--allgather", choices=("oneshot", "rccl"), default="oneshot",
+                    help="row-split exchange: one-shot IPC all-gather (exchange.OneShotAllGather; verified "
+                         "against RCCL at setup, RCCL on any failure) or RCCL all_gather_into_tensor")
     ap.add_argument("--compute-dtype", choices=("fp32", "fp16"), default="fp32",
                     help="Linear4bit compute_dtype: fp32 = the reference default (fp16 x decoded against the "
                          "exact fp32 codes); fp16 = the fp16-rounded code table")
@@ -885,6 +909,9 @@ def main():
         if dist.get_world_size() != args.gpus:
             log(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
             sys.exit(2)
+    gatherer, exchange = None, ("rccl" if sharded else None)
+    if sharded and args.allgather == "oneshot":
+        gatherer, exchange = setup_oneshot(rank)
 
     if args.gemv_only:
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
@@ -914,7 +941,8 @@ def main():
                                  dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16,
                                  compute_dtype=cdt)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
-                                                     layer_ops=layer_ops)
+                                                     layer_ops=layer_ops,
+                                                     gatherer=gatherer if tp_mode == "gather" else None)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1002,7 +1030,7 @@ def main():
 
     layer = None
     if not args.no_roofline:
-        layer = rowsplit_layer(rank, world, sharded)   # every rank takes part (the all-gather)
+        layer = rowsplit_layer(rank, world, sharded, gatherer=gatherer)   # every rank takes part (the all-gather)
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:
@@ -1036,6 +1064,8 @@ def main():
             "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         line["config"]["compute_dtype"] = args.compute_dtype
+        if exchange is not None:
+            line["config"]["exchange"] = exchange
         if extra_codes is not None:
             line["decode_other_codes"] = extra_codes
         if layer is not None:

@@ -217,6 +217,29 @@ int qz_bench_read_floor(const void *p, long long bytes, unsigned int *sink, void
  * period every dependent launch on a stream pays (dispatch + end of kernel). */
 int qz_bench_empty(unsigned int *sink, void *stream);
 
+/* ---- one-shot all-gather over xGMI (the row-split output exchange) ----
+ * Replaces the RCCL all_gather_into_tensor behind parallel.RowShardedLinear4bit (no reference
+ * counterpart: the reference is single-GPU).  Each rank allocates one exchange buffer of
+ * qz_exchange_bytes(world, slot_bytes) bytes with qz_exchange_alloc (uncached device memory),
+ * exports it with qz_ipc_get_handle (qz_ipc_handle_size() bytes), and maps the peers' buffers
+ * with qz_ipc_open_handle (after qz_enable_peer_access to every peer device).  One
+ * qz_allgather_oneshot launch then writes the world x nbytes shards of every rank, rank-major,
+ * into dst (the layout all_gather_into_tensor produces).  epoch: a zeroed device u32 per buffer,
+ * advanced by every launch (graph-capturable); status: a zeroed device u32 set to 1 if a peer's
+ * signal never arrived (bounded wait, ~1 s).  nbytes % 16 == 0, nbytes <= slot_bytes,
+ * 16-B aligned src/dst, world <= 8. */
+int qz_ipc_handle_size(void);
+long long qz_exchange_bytes(int world, long long slot_bytes);
+int qz_exchange_alloc(long long bytes, void **ptr);
+int qz_exchange_free(void *ptr);
+int qz_ipc_get_handle(const void *ptr, void *handle);
+int qz_ipc_open_handle(const void *handle, void **ptr);
+int qz_ipc_close_handle(void *ptr);
+int qz_enable_peer_access(int peer_device);
+int qz_allgather_oneshot(const void *src, int nbytes, void *dst, int rank, int world, void *const *peer_bufs,
+                         void *own_buf, long long slot_bytes, unsigned int *epoch, unsigned int *status,
+                         void *stream);
+
 /* ---- the Linear4bit's callers in a Llama decoder layer (integration.fuse_layer_ops) ----
  * Neither op is in the reference (it leaves them to transformers); they are
  * one-launch restatements of the torch code around the 4-bit projections, with

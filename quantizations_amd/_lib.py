@@ -73,9 +73,18 @@ SIGNATURES = {
     "qz_add_rmsnorm": [_p, _p, _i, _ll, _i, _ll, _p, _f, _p, _p, _ll, _p],
     "qz_bench_read_floor": [_p, _ll, _p, _p],
     "qz_bench_empty": [_p, _p],
+    "qz_ipc_handle_size": [],
+    "qz_exchange_bytes": [_i, _ll],
+    "qz_exchange_alloc": [_ll, _p],
+    "qz_exchange_free": [_p],
+    "qz_ipc_get_handle": [_p, _p],
+    "qz_ipc_open_handle": [_p, _p],
+    "qz_ipc_close_handle": [_p],
+    "qz_enable_peer_access": [_i],
+    "qz_allgather_oneshot": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _p],
     "qz_version": [],
 }
-RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll}
+RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll}
 
 
 def _load():

@@ -1,0 +1,119 @@
+"""One-shot all-gather of row-split decode outputs over xGMI (the RCCL
+replacement the round-2 review asked for).
+
+``OneShotAllGather`` owns this rank's exchange buffer (uncached device memory), maps every
+peer's buffer through hipIpc handles (exchanged once over the process group) and runs one
+``qz_allgather_oneshot`` launch per all-gather (comm.hip): each rank stores its shard straight
+into every peer's buffer, signals with an epoch flag, waits for the peers' flags and unpacks
+the rank-major result -- no collective library, no host round trip, HIP-graph capturable.
+
+It is selected per model by ``parallel.shard_model_linear4bit(..., gatherer=...)``; anything
+it does not take (payloads above its slot, not 16-B multiples, CPU tensors) goes to
+``dist.all_gather_into_tensor`` as before.  ``verify`` compares it with RCCL on live data
+once at setup (bench.py does, and falls back to RCCL on any mismatch).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import check, lib
+
+
+class OneShotAllGather:
+    """All-gather of up to `slot_bytes` per rank, rank-major output (the order of
+    ``dist.all_gather_into_tensor``), through IPC-mapped peer buffers."""
+
+    def __init__(self, group=None, slot_bytes: int = 1 << 16, device: Optional[torch.device] = None):
+        if slot_bytes % 16 != 0 or slot_bytes <= 0:
+            raise ValueError("slot_bytes must be a positive multiple of 16")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > 8:
+            raise ValueError("OneShotAllGather supports up to 8 ranks (one MI355X node)")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.slot_bytes = int(slot_bytes)
+        nbytes = int(lib.qz_exchange_bytes(self.world, self.slot_bytes))
+        own = ctypes.c_void_p()
+        check(lib.qz_exchange_alloc(nbytes, ctypes.byref(own)), "qz_exchange_alloc")
+        self._own = own
+        self._opened = []
+        hsz = int(lib.qz_ipc_handle_size())
+        handle = (ctypes.c_char * hsz)()
+        check(lib.qz_ipc_get_handle(own, handle), "qz_ipc_get_handle")
+        mine = (bytes(handle), self.device.index)
+        allh = [None] * self.world
+        dist.all_gather_object(allh, mine, group=group)
+        peers = (ctypes.c_void_p * self.world)()
+        for r, (h, dev) in enumerate(allh):
+            if r == self.rank:
+                peers[r] = own.value
+                continue
+            check(lib.qz_enable_peer_access(int(dev)), f"qz_enable_peer_access({dev})")
+            p = ctypes.c_void_p()
+            check(lib.qz_ipc_open_handle(ctypes.create_string_buffer(h, hsz), ctypes.byref(p)),
+                  f"qz_ipc_open_handle(rank {r})")
+            self._opened.append(p)
+            peers[r] = p.value
+        self._peers = peers
+        self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        dist.barrier(group=group)   # every rank has mapped every buffer before the first launch
+
+    def accepts(self, inp: torch.Tensor) -> bool:
+        n = inp.numel() * inp.element_size()
+        return (inp.is_cuda and inp.is_contiguous() and n % 16 == 0 and n <= self.slot_bytes
+                and inp.data_ptr() % 16 == 0)
+
+    def __call__(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out[world * n] <- every rank's inp[n], rank-major (all_gather_into_tensor(out, inp))."""
+        n = inp.numel() * inp.element_size()
+        if out.numel() * out.element_size() != self.world * n or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor of world x inp's bytes")
+        check(lib.qz_allgather_oneshot(inp.data_ptr(), n, out.data_ptr(), self.rank, self.world, self._peers,
+                                       self._own, self.slot_bytes, self.epoch.data_ptr(), self.status.data_ptr(),
+                                       _lib.stream_of(inp)), "qz_allgather_oneshot")
+
+    def failed(self) -> bool:
+        """True if any launch so far timed out waiting for a peer (synchronises)."""
+        return bool(self.status.item())
+
+    def verify(self, sizes=(256, 2048, 14336), dtype=torch.float16) -> bool:
+        """Compare with dist.all_gather_into_tensor on this group for a few payload sizes
+        (elements), twice each (both slot parities).  True if every result is identical."""
+        ok = True
+        g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
+        for n in sizes:
+            for _ in range(2):
+                x = torch.randn(n, device=self.device, generator=g).to(dtype)
+                if not self.accepts(x):
+                    continue
+                a = torch.empty(self.world * n, device=self.device, dtype=dtype)
+                b = torch.empty_like(a)
+                self(a, x)
+                dist.all_gather_into_tensor(b, x, group=self.group)
+                ok = ok and bool(torch.equal(a, b))
+        flag = torch.tensor([int(ok and not self.failed())], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
+    def close(self) -> None:
+        for p in self._opened:
+            lib.qz_ipc_close_handle(p)
+        self._opened = []
+        if self._own is not None:
+            lib.qz_exchange_free(self._own)
+            self._own = None
+
+
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, gatherer=None) -> None:
+    """dist.all_gather_into_tensor(out, inp), through `gatherer` when it takes the payload."""
+    if gatherer is not None and gatherer.accepts(inp):
+        gatherer(out, inp)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)

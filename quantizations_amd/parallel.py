@@ -9,7 +9,8 @@ re-quantised, so every rank multiplies exactly the single-GPU layer's weights
 differs).
 x is replicated; after the local fused GEMV/GEMM the fp16 row shards are
 exchanged with ``all_gather_into_tensor`` (RCCL over xGMI on MI355X, gloo in
-the CPU tests).  The reference has no multi-GPU path; this is the build's
+the CPU tests), or -- with a ``gatherer`` (exchange.OneShotAllGather) -- by one
+launch that stores every shard straight into the peers' IPC-mapped buffers.  The reference has no multi-GPU path; this is the build's
 (SURVEY.md section 8e).
 """
 from __future__ import annotations
@@ -22,6 +23,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .core import QuantState, exact_codes_for
+from .exchange import all_gather_into
 
 
 @dataclass
@@ -73,9 +75,10 @@ class RowShardedLinear4bit(nn.Module):
     output on every rank: local fused 4-bit matmul, then an all-gather."""
 
     def __init__(self, full: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 group=None, local_matmul: Optional[Callable] = None, gather: bool = True):
+                 group=None, local_matmul: Optional[Callable] = None, gather: bool = True, gatherer=None):
         super().__init__()
         self.gather = gather  # False: column-parallel (Megatron), the output stays this rank's shard
+        self.gatherer = gatherer  # None: dist.all_gather_into_tensor; else e.g. exchange.OneShotAllGather
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world_size = dist.get_world_size(group) if world_size is None else world_size
         self.group = group
@@ -120,7 +123,7 @@ class RowShardedLinear4bit(nn.Module):
         y2 = y.reshape(-1, rows).contiguous()
         T = y2.shape[0]
         gathered = torch.empty((self.world_size * T, rows), dtype=y.dtype, device=y.device)
-        dist.all_gather_into_tensor(gathered, y2, group=self.group)
+        all_gather_into(gathered, y2, self.group, self.gatherer)
         if T == 1:
             return gathered.reshape(*lead, self.world_size * rows)
         full = gathered.view(self.world_size, T, rows).permute(1, 0, 2).reshape(T, self.world_size * rows)
@@ -151,7 +154,7 @@ def _sharded_group_tokens(group, x: torch.Tensor):
     P = ms[0].world_size
     buf = torch.cat([o.reshape(T, r) for o, r in zip(outs, rows)], dim=1).contiguous()   # [T, S]
     gathered = torch.empty((P * T, S), dtype=buf.dtype, device=buf.device)
-    dist.all_gather_into_tensor(gathered, buf, group=ms[0].group)
+    all_gather_into(gathered, buf, ms[0].group, ms[0].gatherer)
     gathered = gathered.view(P, T, S)
     res, o = [], 0
     for r in rows:
@@ -189,7 +192,7 @@ def sharded_group_compute(group, x: torch.Tensor):
         return [v.view(*lead, r) for v, r in zip(views, rows)]
     P = ms[0].world_size
     gathered = torch.empty(P * S, dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(gathered, buf, group=ms[0].group)
+    all_gather_into(gathered, buf, ms[0].group, ms[0].gatherer)
     g2 = gathered.view(P, S)
     outs, o = [], 0
     for r in rows:
@@ -319,14 +322,16 @@ def apply_tensor_parallel(model: nn.Module, rank: Optional[int] = None, world_si
 
 
 def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                           group=None, local_matmul: Optional[Callable] = None) -> nn.Module:
+                           group=None, local_matmul: Optional[Callable] = None, gatherer=None) -> nn.Module:
     """Replace every Linear4bit of `model` by its RowShardedLinear4bit (row split +
-    all-gather: the north-star multi-GPU layout)."""
+    all-gather: the north-star multi-GPU layout).  `gatherer`: the
+    exchange every layer uses (None = dist.all_gather_into_tensor)."""
     from .modules import Linear4bit
 
     for name, child in list(model.named_children()):
         if isinstance(child, Linear4bit):
-            model._modules[name] = RowShardedLinear4bit(child, rank, world_size, group, local_matmul)
+            model._modules[name] = RowShardedLinear4bit(child, rank, world_size, group, local_matmul,
+                                                        gatherer=gatherer)
         else:
-            shard_model_linear4bit(child, rank, world_size, group, local_matmul)
+            shard_model_linear4bit(child, rank, world_size, group, local_matmul, gatherer)
     return model

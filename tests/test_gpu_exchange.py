@@ -1,0 +1,91 @@
+"""GPU: the one-shot all-gather (comm.hip k_allgather_oneshot through exchange.OneShotAllGather)
+between two processes -- two ranks on the box's one MI355X, each mapping the other's
+uncached exchange buffer through a hipIpc handle (on an 8-GPU node the same code maps
+the peers' buffers over xGMI).  Every call's rank-major result equals the concatenation
+of both ranks' shards, over payload sizes from 16 B to the slot size, both slot parities,
+eager launches and a HIP-graph replay; no wait ever times out."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+from test_distributed import _free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _shard(rank, call, n):
+    g = torch.Generator().manual_seed(1000 * call + rank)
+    return torch.randn(n, generator=g).half()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        from quantizations_amd.exchange import OneShotAllGather
+
+        dev = torch.device("cuda", 0)
+        ag = OneShotAllGather(slot_bytes=1 << 16, device=dev)
+        bad = []
+        sizes = [8, 16, 1024, 7168, 32768, 8, 4096, 14336]     # fp16 elements: 16 B .. 64 KiB
+        for call in range(24):
+            n = sizes[call % len(sizes)]
+            x = _shard(rank, call, n).to(dev)
+            out = torch.empty(world * n, dtype=torch.float16, device=dev)
+            ag(out, x)
+            exp = torch.cat([_shard(r, call, n) for r in range(world)])
+            if not torch.equal(out.cpu(), exp):
+                bad.append(call)
+        # graph capture: fixed buffers, four calls per replay
+        n = 2048
+        xs = [torch.empty(n, dtype=torch.float16, device=dev) for _ in range(4)]
+        outs = [torch.empty(world * n, dtype=torch.float16, device=dev) for _ in range(4)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        dist.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for x, o in zip(xs, outs):
+                ag(o, x)
+        torch.cuda.synchronize()
+        for rep in range(3):
+            for i, x in enumerate(xs):
+                x.copy_(_shard(rank, 100 + 10 * rep + i, n))
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            for i, o in enumerate(outs):
+                exp = torch.cat([_shard(r, 100 + 10 * rep + i, n) for r in range(world)])
+                if not torch.equal(o.cpu(), exp):
+                    bad.append(("graph", rep, i))
+        q.put((rank, bad, ag.failed(), int(ag.epoch.item())))
+        dist.barrier()
+        ag.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_oneshot_allgather_two_processes_one_gpu():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
+        os.environ.get("PYTHONPATH", "")
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, bad, failed, epoch in res:
+        assert not failed, f"rank {rank}: a peer's signal timed out"
+        assert not bad, f"rank {rank}: wrong all-gather results at {bad}"
+        assert epoch == 24 + 3 * 4, epoch   # 24 eager calls + 3 replays x 4 (capture runs nothing)

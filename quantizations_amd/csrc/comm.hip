@@ -7,11 +7,13 @@
 // (one workgroup) per all-gather:
 //   1. push: the rank's shard (the GEMV output) is stored into slot [parity][rank] of EVERY
 //      rank's buffer, its own included -- remote stores go straight over xGMI;
-//   2. signal: after its stores have completed (vmcnt(0), workgroup barrier, system-scope
-//      release fence), one lane per peer stores the call's epoch into flag [parity][rank] of
-//      that peer's buffer (system scope);
+//   2. signal: after its stores have completed (vmcnt(0), workgroup barrier), one lane per peer
+//      stores the call's epoch into flag [parity][rank] of that peer's buffer (system scope);
+//      every byte a peer reads lives in uncached memory, so no cache write-back (release
+//      fence) is needed -- only the stores' completion;
 //   3. wait: one lane per peer polls flag [parity][peer] of the OWN buffer (system-scope loads,
-//      bounded spin: a peer that never arrives sets the status word instead of hanging the GPU);
+//      bounded spin: a peer that never arrives sets the status word instead of hanging the GPU),
+//      then the uncached slots are read (no cache to invalidate);
 //   4. unpack: the world x nbytes slots are copied into the output tensor (ordinary memory, so
 //      the consumers of the gathered activation read it through the caches as usual).
 // The epoch is a device-side counter (read at entry, advanced at exit by the same launch), so
@@ -63,11 +65,10 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_oneshot(AllGatherParam
   // 2. every store of this workgroup has completed, then the epoch goes to each peer
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid < p.world) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (no release fence: the shard went to UNCACHED memory, so no cache holds anything a peer
+  // must see -- a fence's L2 write-back would only flush unrelated dirty lines, ~2 us)
+  if (tid < p.world)
     __hip_atomic_store(ag_flag(p.peer[tid], par, p.rank), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
   // 3. wait for every peer's epoch in the own buffer (bounded: ~1 s, then report and go on)
   if (tid < p.world) {
     unsigned int *f = ag_flag(p.own, par, tid);
@@ -79,7 +80,6 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_oneshot(AllGatherParam
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
   }
   __syncthreads();
   // 4. unpack the world slots (uncached) into the output

@@ -780,18 +780,29 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
 
+  // ABL & 32768 (microbenchmark, timing only: WRONG outputs): a prologue without memory -- the
+  // byte table from the SGPR planes, code2 / offset replaced by constants -- to price the
+  // prologue's global loads (which queue behind the CU's HBM requests)
+  constexpr bool kNoPro = (ABL & 32768) != 0;
   // 1. the double-quant code table load goes out first (it gates the barrier)
   float c2 = 0.0f, offset = 0.0f;
-  if constexpr (DQ) {
+  if constexpr (DQ && !kNoPro) {
     if (NW * 64 == 256 || threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x & 255];
     offset = *p.sc.offset;
+  } else if constexpr (DQ) {
+    c2 = (float)(threadIdx.x & 255) * (1.0f / 256.0f);
   }
   // 1b. the precomputed byte-table entry of this thread (issued before the
   // weights, so waiting for it does not wait for the first HBM step)
-  // 1b. the precomputed byte-table entry of this thread (issued before the
-  // weights, so waiting for it does not wait for the first HBM step)
   u32x4 tab_entry = {0u, 0u, 0u, 0u};
-  if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
+  if constexpr (kNoPro && MODE == kModeTab) {
+    uint32_t P[4], tp[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tp[i] = p.tab[i];
+    decode_lut16((uint32_t)threadIdx.x, tp, P);
+    const uint32_t h = (P[0] & 0xFFFFu) | (P[2] << 16);
+    tab_entry = u32x4{h, h, h, h};
+  } else if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
     if (!p.lut && threadIdx.x < 256) {
       const ByteTable *bt = kF32  ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)

@@ -371,6 +371,20 @@ int main(int argc, char **argv) {
     GVN(1, true, 4, 2, 8); GVN(1, true, 4, 4, 8); GVN(1, true, 2, 2, 8); GVN(1, true, 4, 1, 8);
     GVN(1, true, 2, 1, 8); GVN(1, true, 4, 8, 8);
   }
+  const bool nopro = argc > 4 && std::string(argv[4]) == "nopro";
+  if (nopro) {  // price of the prologue's global loads (ABL 32768: timing only, wrong outputs)
+    GVFS(2, 0); GVFS(2, 32768); GVFS(4, 0); GVFS(4, 32768); GVFS(1, 0); GVFS(1, 32768);
+  }
+  const bool wt8 = argc > 4 && std::string(argv[4]) == "wt8";
+#define GVWN(R, NW, CL_, WT_) timeit("gemvFS R=" #R " NW=" #NW " CL=" #CL_ " WT=" #WT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * NW - 1) / (R * NW)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, NW, false, 0, true, CL_, WT_>), dim3(g), dim3(NW * 64), 0, 0, q); })
+  if (wt8) {  // exact codes: conflict-free 64 KiB table (WT) shared by 8 waves vs the 16-copy table at 4 waves
+    GVWN(4, 4, false, false); GVWN(4, 4, true, false); GVWN(4, 8, true, true); GVWN(4, 4, true, true);
+    GVWN(2, 4, false, false); GVWN(2, 4, true, false); GVWN(2, 8, true, true); GVWN(2, 8, true, false);
+    GVWN(1, 8, true, true);
+  }
   const bool stream = argc > 4 && std::string(argv[4]) == "stream";
 #define GVST(R, G, CL_) timeit("stream2 R=" #R " wgs=" #G " CL=" #CL_, [&, pt = p](int i) { \
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
@@ -384,7 +398,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

@@ -34,10 +34,12 @@
 //    weight, half of them half-rate v_perm: VALU-issue-bound on gfx950.
 // Products: v_dot2_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
 // per 32-element chunk the fp32 dot is scaled by the block absmax with one
-// FMA.  fp32/bf16 activations are split into hi+lo fp16 halves (x = xh + xl)
-// after a per-lane power-of-two pre-scale that puts the chunk's largest |x| in
-// [2^14, 2^15): no saturation above 65504, no flush below 2^-24, ~2^-21 of
-// the chunk maximum (undone exactly on the fp32 dot).
+// FMA.  On the product byte-table path bf16 x is dotted RAW against bf16 hi + lo
+// code pairs (v_dot2c_f32_bf16, kRawBF) and fp32 x RAW against fp32 codes
+// (v_fma_f32, kRawF32): no conversion of x.  Only the register-decode modes
+// (microbenchmarks) still split fp32/bf16 x into hi+lo fp16 halves after a
+// per-lane power-of-two pre-scale that puts the chunk's largest |x| in
+// [2^14, 2^15) (kScaled; undone exactly on the fp32 dot).
 // Exact codes (CL): a runtime codebook (`lut`, the reference ABI's fp32
 // quant_map, kernels.cu:1115-1120) is NOT rounded to fp16: each code c is
 // stored as c * 2^S = ch + cl, two fp16 values (~2^-23 relative: fp32-class),

@@ -224,10 +224,11 @@ int qz_bench_empty(unsigned int *sink, void *stream);
  * exports it with qz_ipc_get_handle (qz_ipc_handle_size() bytes), and maps the peers' buffers
  * with qz_ipc_open_handle (after qz_enable_peer_access to every peer device).  One
  * qz_allgather_oneshot launch then writes the world x nbytes shards of every rank, rank-major,
- * into dst (the layout all_gather_into_tensor produces).  epoch: a zeroed device u32 per buffer,
- * advanced by every launch (graph-capturable); status: a zeroed device u32 set to 1 if a peer's
- * signal never arrived (bounded wait, ~1 s).  nbytes % 16 == 0, nbytes <= slot_bytes,
- * 16-B aligned src/dst, world <= 8. */
+ * into dst (the layout all_gather_into_tensor produces); the shard words travel as 8-byte
+ * {word, epoch} granules (one system-scope store each, read once tagged with the call's epoch).
+ * epoch: a zeroed device u32[2] per buffer (epoch, ticket), advanced by every launch
+ * (graph-capturable); status: a zeroed device u32 set to 1 if a peer's granules never arrived
+ * (bounded wait).  nbytes % 16 == 0, nbytes <= slot_bytes, 16-B aligned src/dst, world <= 8. */
 int qz_ipc_handle_size(void);
 long long qz_exchange_bytes(int world, long long slot_bytes);
 int qz_exchange_alloc(long long bytes, void **ptr);
@@ -239,6 +240,12 @@ int qz_enable_peer_access(int peer_device);
 int qz_allgather_oneshot(const void *src, int nbytes, void *dst, int rank, int world, void *const *peer_bufs,
                          void *own_buf, long long slot_bytes, unsigned int *epoch, unsigned int *status,
                          void *stream);
+/* The same with the protocol forced: mode 1 = flag protocol (16-B stores into plain slots,
+ * a store-completion wait, one epoch flag per peer), 2 = tagged granules.  qz_allgather_oneshot
+ * takes granules up to 2 KiB per rank and flags above (measured). */
+int qz_allgather_oneshot_mode(const void *src, int nbytes, void *dst, int rank, int world, void *const *peer_bufs,
+                              void *own_buf, long long slot_bytes, unsigned int *epoch, unsigned int *status,
+                              int mode, void *stream);
 
 /* ---- the Linear4bit's callers in a Llama decoder layer (integration.fuse_layer_ops) ----
  * Neither op is in the reference (it leaves them to transformers); they are

@@ -82,6 +82,7 @@ SIGNATURES = {
     "qz_ipc_close_handle": [_p],
     "qz_enable_peer_access": [_i],
     "qz_allgather_oneshot": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _p],
+    "qz_allgather_oneshot_mode": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _i, _p],
     "qz_version": [],
 }
 RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll}

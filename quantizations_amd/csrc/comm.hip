@@ -3,73 +3,96 @@
 //
 // Every rank owns one exchange buffer in UNCACHED device memory (hipDeviceMallocUncached: no
 // cache of any GPU holds its lines, so a peer's store over xGMI is what the owner's next load
-// sees) and maps its peers' buffers through hipIpc handles.  One launch of k_allgather_oneshot
-// (one workgroup) per all-gather:
-//   1. push: the rank's shard (the GEMV output) is stored into slot [parity][rank] of EVERY
-//      rank's buffer, its own included -- remote stores go straight over xGMI;
-//   2. signal: after its stores have completed (vmcnt(0), workgroup barrier), one lane per peer
-//      stores the call's epoch into flag [parity][rank] of that peer's buffer (system scope);
-//      every byte a peer reads lives in uncached memory, so no cache write-back (release
-//      fence) is needed -- only the stores' completion;
-//   3. wait: one lane per peer polls flag [parity][peer] of the OWN buffer (system-scope loads,
-//      bounded spin: a peer that never arrives sets the status word instead of hanging the GPU),
-//      then the uncached slots are read (no cache to invalidate);
-//   4. unpack: the world x nbytes slots are copied into the output tensor (ordinary memory, so
-//      the consumers of the gathered activation read it through the caches as usual).
-// The epoch is a device-side counter (read at entry, advanced at exit by the same launch), so
-// the launch is HIP-graph capturable with fixed arguments.  Slots alternate by epoch parity: a
-// peer can be at most one call ahead (it cannot finish call e+1 before this rank has signalled
-// e+1, i.e. finished call e), so call e+1's pushes never land in the slots call e still reads.
+// sees) and maps its peers' buffers through hipIpc handles.  The payload travels as TAGGED
+// GRANULES: every 4-byte word of a shard is stored as one 8-byte {word, epoch} granule by a
+// single 8-byte system-scope store, so a reader knows a word has arrived when its tag equals
+// the call's epoch -- no separate flag, no store-completion wait, no cache fence, one xGMI
+// trip per word (the guide's granule hand-off, MI355X_MICROARCH.md price list).
+// Payloads up to QZ_AG_GRANULE_MAX_BYTES: one launch of k_allgather_granules, one 1024-thread
+// workgroup per rank (larger payloads: k_allgather_flags below):
+//   1. push: workgroup b stores granules of words [b, b + 1) * nwords / world of this rank's
+//      shard into region [parity][rank] of EVERY rank's buffer (its own included);
+//   2. pull: workgroup b polls the granules of rank b's region in the OWN buffer (all of a
+//      thread's loads in flight at once, re-polling the ones not yet tagged; bounded: a peer
+//      that never arrives sets the status word instead of hanging the GPU) and writes the
+//      words into the output (ordinary memory), rank-major.
+// The epoch is a device-side counter: every workgroup reads it at entry and the last one to
+// finish (an agent-scope ticket) advances it, so the launch is HIP-graph capturable with fixed
+// arguments.  Regions alternate by epoch parity: a peer can be at most one call ahead (it cannot
+// finish call e+1 before this rank has pushed e+1, i.e. finished call e), so call e+1's granules
+// never land in the region call e still reads; a stale granule there carries epoch e-1 or e-2.
 #include <cstring>
 
 #include "common.h"
 
+#ifndef QZ_AG_GRANULE_MAX_BYTES
+#define QZ_AG_GRANULE_MAX_BYTES 2048
+#endif
+
 namespace qz {
 
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr int kAgThreads = 1024;
 constexpr int kAgMaxWorld = 8;
-constexpr int kAgFlagBytes = 256;   // flags [2][32] u32 (one 128-B line per parity) at the buffer's head
+constexpr int kAgHeadBytes = 256;   // buffer head: the flags [2][32] u32 of the flag protocol
+constexpr int kAgPoll = 8;          // granules per thread per polling round
 
 struct AllGatherParams {
   const void *src;                    // this rank's shard, nbytes (16-B aligned)
   void *dst;                          // world * nbytes, rank-major (all_gather_into_tensor order)
   unsigned char *peer[kAgMaxWorld];   // every rank's exchange buffer, mapped here (own included)
   unsigned char *own;                 // this rank's exchange buffer
-  unsigned int *epoch;                // device counter (ordinary memory)
-  unsigned int *status;               // 0 = ok; 1 = a peer's flag never arrived
-  long long slot_bytes;               // bytes per (parity, rank) slot
+  unsigned int *epoch;                // device counter (ordinary memory) + ticket at epoch[1]
+  unsigned int *status;               // 0 = ok; 1 = a peer's granules never arrived
+  long long slot_bytes;               // payload bytes per (parity, rank) region (granules: 2x)
   int nbytes, rank, world;
 };
 
-__device__ __forceinline__ unsigned int *ag_flag(unsigned char *buf, int par, int r) {
-  return reinterpret_cast<unsigned int *>(buf) + par * 32 + r;
+// granule i of rank q's region, parity par, in buffer buf
+__device__ __forceinline__ unsigned long long *ag_granule(unsigned char *buf, int par, int q, int world,
+                                                         long long slot_bytes) {
+  return reinterpret_cast<unsigned long long *>(buf + kAgHeadBytes + ((long long)par * world + q) * 2 * slot_bytes);
+}
+// flag protocol: rank q's plain slot (after all granule regions) and its flag, parity par
+__device__ __forceinline__ unsigned char *ag_slot(unsigned char *buf, int par, int q, int world, long long slot_bytes) {
+  return buf + kAgHeadBytes + 4LL * world * slot_bytes + ((long long)par * world + q) * slot_bytes;
+}
+__device__ __forceinline__ unsigned int *ag_flag(unsigned char *buf, int par, int q) {
+  return reinterpret_cast<unsigned int *>(buf) + par * 32 + q;
+}
+// the last workgroup of a launch to finish advances the epoch (all have read it by then)
+__device__ __forceinline__ void ag_advance_epoch(unsigned int *ep, unsigned int epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int t = __hip_atomic_fetch_add(ep + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (unsigned int)(gridDim.x - 1)) {
+      __hip_atomic_store(ep + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
-__global__ __launch_bounds__(kAgThreads) void k_allgather_oneshot(AllGatherParams p) {
+// Flag protocol (large payloads: 16-B stores, half the bytes of the granules, but one more
+// xGMI trip): one workgroup stores the shard into slot [parity][rank] of every rank, waits for
+// the stores' completion, stores the epoch into each rank's flag [parity][rank] (system scope),
+// polls its own flags, then copies the world slots out.  No cache fence: all of it is uncached.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kAgThreads) void k_allgather_flags(AllGatherParams p) {
   const int tid = threadIdx.x;
-  const unsigned int epoch = *p.epoch + 1u;
+  const unsigned int epoch = p.epoch[0] + 1u;
   const int par = (int)(epoch & 1u);
   const int n16 = p.nbytes >> 4;
-  const long long slot0 = kAgFlagBytes + (long long)par * p.world * p.slot_bytes;
-  // 1. push the shard into every rank's slot [par][rank]
   const v4u *src = reinterpret_cast<const v4u *>(p.src);
   for (int i = tid; i < n16; i += kAgThreads) {
     const v4u v = src[i];
 #pragma unroll
     for (int r = 0; r < kAgMaxWorld; ++r) {
-      if (r < p.world)
-        reinterpret_cast<v4u *>(p.peer[r] + slot0 + (long long)p.rank * p.slot_bytes)[i] = v;
+      if (r < p.world) reinterpret_cast<v4u *>(ag_slot(p.peer[r], par, p.rank, p.world, p.slot_bytes))[i] = v;
     }
   }
-  // 2. every store of this workgroup has completed, then the epoch goes to each peer
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // (no release fence: the shard went to UNCACHED memory, so no cache holds anything a peer
-  // must see -- a fence's L2 write-back would only flush unrelated dirty lines, ~2 us)
   if (tid < p.world)
     __hip_atomic_store(ag_flag(p.peer[tid], par, p.rank), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // 3. wait for every peer's epoch in the own buffer (bounded: ~1 s, then report and go on)
   if (tid < p.world) {
     unsigned int *f = ag_flag(p.own, par, tid);
     long long spins = 0;
@@ -82,20 +105,77 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_oneshot(AllGatherParam
     }
   }
   __syncthreads();
-  // 4. unpack the world slots (uncached) into the output
   v4u *dst = reinterpret_cast<v4u *>(p.dst);
-  const int total = n16 * p.world;
-  for (int i = tid; i < total; i += kAgThreads) {
+  for (int i = tid; i < n16 * p.world; i += kAgThreads) {
     const int r = i / n16, j = i - r * n16;
-    dst[i] = reinterpret_cast<const v4u *>(p.own + slot0 + (long long)r * p.slot_bytes)[j];
+    dst[i] = reinterpret_cast<const v4u *>(ag_slot(p.own, par, r, p.world, p.slot_bytes))[j];
   }
-  // 5. the next call's epoch (every thread has read this one: the barrier above)
-  if (tid == 0) *p.epoch = epoch;
+  ag_advance_epoch(p.epoch, epoch);
+}
+
+__global__ __launch_bounds__(kAgThreads) void k_allgather_granules(AllGatherParams p) {
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const unsigned int epoch = p.epoch[0] + 1u;
+  const int par = (int)(epoch & 1u);
+  const int nw = p.nbytes >> 2;
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  // 1. push words [w0, w1) of the shard to every rank, one 8-byte {word, epoch} store each
+  const unsigned int *src = reinterpret_cast<const unsigned int *>(p.src);
+  const int w0 = (int)((long long)nw * b / p.world), w1 = (int)((long long)nw * (b + 1) / p.world);
+  for (int i = w0 + tid; i < w1; i += kAgThreads) {
+    const unsigned long long g = tag | src[i];
+#pragma unroll
+    for (int r = 0; r < kAgMaxWorld; ++r) {
+      if (r < p.world)
+        __hip_atomic_store(ag_granule(p.peer[r], par, p.rank, p.world, p.slot_bytes) + i, g, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // 2. pull rank b's words from the own buffer once their tags say this epoch
+  unsigned long long *in = ag_granule(p.own, par, b, p.world, p.slot_bytes);
+  unsigned int *dst = reinterpret_cast<unsigned int *>(p.dst) + (long long)b * nw;
+  for (int base = tid; base < nw; base += kAgPoll * kAgThreads) {
+    unsigned long long g[kAgPoll];
+#pragma unroll
+    for (int k = 0; k < kAgPoll; ++k) {
+      const int i = base + k * kAgThreads;
+      g[k] = i < nw ? __hip_atomic_load(in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : tag;
+    }
+    long long spins = 0;
+    for (;;) {
+      bool all = true;
+#pragma unroll
+      for (int k = 0; k < kAgPoll; ++k) {
+        const int i = base + k * kAgThreads;
+        if ((g[k] >> 32) != epoch) {
+          all = false;
+          g[k] = __hip_atomic_load(in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if (all) break;
+      if (++spins > (1LL << 22)) {
+        __hip_atomic_store(p.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int k = 0; k < kAgPoll; ++k) {
+      const int i = base + k * kAgThreads;
+      if (i < nw) dst[i] = (unsigned int)g[k];
+    }
+  }
+  // 3. the last workgroup to finish advances the epoch (every workgroup has read it by then)
+  ag_advance_epoch(p.epoch, epoch);
 }
 
 }  // namespace qz
 
 using namespace qz;
+
+extern "C" int qz_allgather_oneshot_mode(const void *src, int nbytes, void *dst, int rank, int world,
+                                         void *const *peer_bufs, void *own_buf, long long slot_bytes,
+                                         unsigned int *epoch, unsigned int *status, int mode, void *stream);
 
 extern "C" int qz_ipc_handle_size(void) { return (int)sizeof(hipIpcMemHandle_t); }
 
@@ -138,9 +218,21 @@ extern "C" int qz_enable_peer_access(int peer_device) {
   return (int)e;
 }
 
+// Payloads up to this size travel as tagged granules (one xGMI trip, 2x the bytes), larger ones
+// by the flag protocol (16-B stores + one flag trip); measured: DESIGN.md section 6.
+constexpr int kAgGranuleMaxBytes = QZ_AG_GRANULE_MAX_BYTES;
+
 extern "C" int qz_allgather_oneshot(const void *src, int nbytes, void *dst, int rank, int world,
                                     void *const *peer_bufs, void *own_buf, long long slot_bytes, unsigned int *epoch,
                                     unsigned int *status, void *stream) {
+  return qz_allgather_oneshot_mode(src, nbytes, dst, rank, world, peer_bufs, own_buf, slot_bytes, epoch, status,
+                                   nbytes <= kAgGranuleMaxBytes ? 2 : 1, stream);
+}
+
+extern "C" int qz_allgather_oneshot_mode(const void *src, int nbytes, void *dst, int rank, int world,
+                                         void *const *peer_bufs, void *own_buf, long long slot_bytes,
+                                         unsigned int *epoch, unsigned int *status, int mode, void *stream) {
+  if (mode != 1 && mode != 2) return QZ_ERR_ARG;
   if (!src || !dst || !peer_bufs || !own_buf || !epoch || !status || nbytes < 0) return QZ_ERR_ARG;
   if (world < 1 || world > kAgMaxWorld || rank < 0 || rank >= world) return QZ_ERR_ARG;
   if (nbytes % 16 != 0 || nbytes > slot_bytes || slot_bytes % 16 != 0 ||
@@ -160,11 +252,15 @@ extern "C" int qz_allgather_oneshot(const void *src, int nbytes, void *dst, int 
   p.nbytes = nbytes;
   p.rank = rank;
   p.world = world;
-  hipLaunchKernelGGL(k_allgather_oneshot, dim3(1), dim3(kAgThreads), 0, (hipStream_t)stream, p);
+  if (mode == 2)
+    hipLaunchKernelGGL(k_allgather_granules, dim3(world), dim3(kAgThreads), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(k_allgather_flags, dim3(1), dim3(kAgThreads), 0, (hipStream_t)stream, p);
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }
 
 extern "C" long long qz_exchange_bytes(int world, long long slot_bytes) {
-  return kAgFlagBytes + 2LL * world * slot_bytes;
+  // flags head + [parity][rank] regions of 8-B granules (2x the payload) + [parity][rank] plain slots
+  return kAgHeadBytes + 2LL * world * 2 * slot_bytes + 2LL * world * slot_bytes;
 }

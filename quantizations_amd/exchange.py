@@ -4,8 +4,9 @@ replacement the round-2 review asked for).
 ``OneShotAllGather`` owns this rank's exchange buffer (uncached device memory), maps every
 peer's buffer through hipIpc handles (exchanged once over the process group) and runs one
 ``qz_allgather_oneshot`` launch per all-gather (comm.hip): each rank stores its shard straight
-into every peer's buffer, signals with an epoch flag, waits for the peers' flags and unpacks
-the rank-major result -- no collective library, no host round trip, HIP-graph capturable.
+into every peer's buffer as 8-byte {word, epoch} granules, and each rank reads the granules
+arriving in its own buffer once their tags carry the call's epoch -- no collective library, no
+flag round trip, no host involvement, HIP-graph capturable.
 
 It is selected per model by ``parallel.shard_model_linear4bit(..., gatherer=...)``; anything
 it does not take (payloads above its slot, not 16-B multiples, CPU tensors) goes to
@@ -61,7 +62,7 @@ class OneShotAllGather:
             self._opened.append(p)
             peers[r] = p.value
         self._peers = peers
-        self.epoch = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.epoch = torch.zeros(2, dtype=torch.int32, device=self.device)   # epoch, last-finisher ticket
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         dist.barrier(group=group)   # every rank has mapped every buffer before the first launch
 
@@ -70,14 +71,18 @@ class OneShotAllGather:
         return (inp.is_cuda and inp.is_contiguous() and n % 16 == 0 and n <= self.slot_bytes
                 and inp.data_ptr() % 16 == 0)
 
-    def __call__(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        """out[world * n] <- every rank's inp[n], rank-major (all_gather_into_tensor(out, inp))."""
+    def __call__(self, out: torch.Tensor, inp: torch.Tensor, mode: int = 0) -> None:
+        """out[world * n] <- every rank's inp[n], rank-major (all_gather_into_tensor(out, inp)).
+        mode: 0 = by payload size (qz_allgather_oneshot), 1 = flag protocol, 2 = tagged granules."""
         n = inp.numel() * inp.element_size()
         if out.numel() * out.element_size() != self.world * n or not out.is_contiguous():
             raise ValueError("out must be a contiguous tensor of world x inp's bytes")
-        check(lib.qz_allgather_oneshot(inp.data_ptr(), n, out.data_ptr(), self.rank, self.world, self._peers,
-                                       self._own, self.slot_bytes, self.epoch.data_ptr(), self.status.data_ptr(),
-                                       _lib.stream_of(inp)), "qz_allgather_oneshot")
+        args = (inp.data_ptr(), n, out.data_ptr(), self.rank, self.world, self._peers, self._own, self.slot_bytes,
+                self.epoch.data_ptr(), self.status.data_ptr())
+        if mode:
+            check(lib.qz_allgather_oneshot_mode(*args, mode, _lib.stream_of(inp)), "qz_allgather_oneshot_mode")
+        else:
+            check(lib.qz_allgather_oneshot(*args, _lib.stream_of(inp)), "qz_allgather_oneshot")
 
     def failed(self) -> bool:
         """True if any launch so far timed out waiting for a peer (synchronises)."""
@@ -93,11 +98,12 @@ class OneShotAllGather:
                 x = torch.randn(n, device=self.device, generator=g).to(dtype)
                 if not self.accepts(x):
                     continue
-                a = torch.empty(self.world * n, device=self.device, dtype=dtype)
-                b = torch.empty_like(a)
-                self(a, x)
+                b = torch.empty(self.world * n, device=self.device, dtype=dtype)
                 dist.all_gather_into_tensor(b, x, group=self.group)
-                ok = ok and bool(torch.equal(a, b))
+                for mode in (0, 1, 2):
+                    a = torch.empty_like(b)
+                    self(a, x, mode)
+                    ok = ok and bool(torch.equal(a, b))
         flag = torch.tensor([int(ok and not self.failed())], device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item())

@@ -28,10 +28,10 @@ def _placement_worker(rank, world, port, q):
 
         from quantizations_amd.exchange import all_gather_into
 
-        ag = ShmAllGather(slot_bytes=4096, tag=f"p{port}")
+        ag = ShmAllGather(slot_bytes=6144, tag=f"p{port}")
         ok, used = True, 0
         g = torch.Generator().manual_seed(rank)
-        for n in (8, 16, 24, 512, 2048, 8, 2048, 4096):       # fp16 elements: 16 B .. 8 KiB
+        for n in (8, 16, 24, 512, 2048, 8, 3072, 2048, 4096):  # fp16 elements: 16 B .. 8 KiB (both protocols)
             x = torch.randn(n, generator=g).half()
             a = torch.empty(world * n, dtype=torch.float16)
             b = torch.empty_like(a)
@@ -61,7 +61,7 @@ def test_oneshot_protocol_placement_and_parity():
         assert p.exitcode == 0
     for rank, ok, used in res:
         assert ok, f"rank {rank}: one-shot result differs from all_gather_into_tensor"
-        assert used == 7, used     # 4096 elements = 8 KiB > the 4 KiB slot: the collective
+        assert used == 8, used     # 4096 elements = 8 KiB > the 6 KiB slot: the collective
 
 
 def _model_worker(rank, world, port, q):

@@ -3,7 +3,8 @@ between two processes -- two ranks on the box's one MI355X, each mapping the oth
 uncached exchange buffer through a hipIpc handle (on an 8-GPU node the same code maps
 the peers' buffers over xGMI).  Every call's rank-major result equals the concatenation
 of both ranks' shards, over payload sizes from 16 B to the slot size, both slot parities,
-eager launches and a HIP-graph replay; no wait ever times out."""
+both protocols (flags, tagged granules) interleaved, eager launches and a HIP-graph replay;
+no wait ever times out."""
 import os
 
 import pytest
@@ -37,7 +38,7 @@ def _worker(rank, world, port, q):
             n = sizes[call % len(sizes)]
             x = _shard(rank, call, n).to(dev)
             out = torch.empty(world * n, dtype=torch.float16, device=dev)
-            ag(out, x)
+            ag(out, x, (0, 1, 2)[call % 3])   # by size, flag protocol, tagged granules
             exp = torch.cat([_shard(r, call, n) for r in range(world)])
             if not torch.equal(out.cpu(), exp):
                 bad.append(call)
@@ -64,7 +65,7 @@ def _worker(rank, world, port, q):
                 exp = torch.cat([_shard(r, 100 + 10 * rep + i, n) for r in range(world)])
                 if not torch.equal(o.cpu(), exp):
                     bad.append(("graph", rep, i))
-        q.put((rank, bad, ag.failed(), int(ag.epoch.item())))
+        q.put((rank, bad, ag.failed(), int(ag.epoch[0].item())))
         dist.barrier()
         ag.close()
     finally:

@@ -159,6 +159,8 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
         with torch.cuda.graph(cg, capture_error_mode=CAPTURE_MODE):
             step()
         run = cg.replay
+        if world > 1:
+            dist.barrier()   # every rank starts replaying together (in-graph exchanges wait on peers)
     for _ in range(warmup):
         run()
     if world > 1:

@@ -228,7 +228,7 @@ int qz_bench_empty(unsigned int *sink, void *stream);
  * {word, epoch} granules (one system-scope store each, read once tagged with the call's epoch).
  * epoch: a zeroed device u32[2] per buffer (epoch, ticket), advanced by every launch
  * (graph-capturable); status: a zeroed device u32 set to 1 if a peer's granules never arrived
- * (bounded wait).  nbytes % 16 == 0, nbytes <= slot_bytes, 16-B aligned src/dst, world <= 8. */
+ * (bounded wait, 5 s).  nbytes % 16 == 0, nbytes <= slot_bytes, 16-B aligned src/dst, world <= 8. */
 int qz_ipc_handle_size(void);
 long long qz_exchange_bytes(int world, long long slot_bytes);
 int qz_exchange_alloc(long long bytes, void **ptr);

@@ -21,6 +21,7 @@ What differs, on purpose (DESIGN.md "Host layer"):
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import json
 import os
@@ -187,6 +188,21 @@ class Params4bit(torch.nn.Parameter):
         if module is not None:
             module.quant_state = qs
         return self
+
+    def __deepcopy__(self, memo):
+        """A copy that keeps the 4-bit state (torch's Parameter.__deepcopy__ would rebuild an
+        un-quantised Params4bit from the packed bytes, as bnb's own Params4bit avoids too): the
+        packed bytes and the QuantState are copied, and the module back-reference follows the
+        module when the whole module is being copied."""
+        if id(self) in memo:
+            return memo[id(self)]
+        new = type(self)(self.data.clone(memory_format=torch.preserve_format), requires_grad=self.requires_grad,
+                         quant_state=copy.deepcopy(self.quant_state, memo), blocksize=self.blocksize,
+                         quant_type=self.quant_type, quant_storage=self.quant_storage,
+                         module=memo.get(id(self.module), self.module), bnb_quantized=self.bnb_quantized,
+                         compress_statistics=self.compress_statistics)
+        memo[id(self)] = new
+        return new
 
     def _quantize(self, device):
         w = self.data.contiguous().to(device)

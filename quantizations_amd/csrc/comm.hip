@@ -13,8 +13,8 @@
 //   1. push: workgroup b stores granules of words [b, b + 1) * nwords / world of this rank's
 //      shard into region [parity][rank] of EVERY rank's buffer (its own included);
 //   2. pull: workgroup b polls the granules of rank b's region in the OWN buffer (all of a
-//      thread's loads in flight at once, re-polling the ones not yet tagged; bounded: a peer
-//      that never arrives sets the status word instead of hanging the GPU) and writes the
+//      thread's loads in flight at once, re-polling the ones not yet tagged; bounded, 5 s: a
+//      peer that never arrives sets the status word instead of hanging the GPU) and writes the
 //      words into the output (ordinary memory), rank-major.
 // The epoch is a device-side counter: every workgroup reads it at entry and the last one to
 // finish (an agent-scope ticket) advances it, so the launch is HIP-graph capturable with fixed
@@ -35,6 +35,10 @@ constexpr int kAgThreads = 1024;
 constexpr int kAgMaxWorld = 8;
 constexpr int kAgHeadBytes = 256;   // buffer head: the flags [2][32] u32 of the flag protocol
 constexpr int kAgPoll = 8;          // granules per thread per polling round
+// a peer that never arrives: give up after 5 s of the 100 MHz s_memrealtime clock (the status
+// word reports it) -- long enough for any rank skew of a healthy job, bounded so a dead peer
+// cannot hang the GPU
+constexpr unsigned long long kAgWaitTicks = 500000000ull;
 
 struct AllGatherParams {
   const void *src;                    // this rank's shard, nbytes (16-B aligned)
@@ -95,10 +99,10 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_flags(AllGatherParams 
     __hip_atomic_store(ag_flag(p.peer[tid], par, p.rank), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < p.world) {
     unsigned int *f = ag_flag(p.own, par, tid);
-    long long spins = 0;
+    const unsigned long long t_give_up = __builtin_amdgcn_s_memrealtime() + kAgWaitTicks;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1LL << 24)) {
+      if (__builtin_amdgcn_s_memrealtime() > t_give_up) {
         __hip_atomic_store(p.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_granules(AllGatherPara
       const int i = base + k * kAgThreads;
       g[k] = i < nw ? __hip_atomic_load(in + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : tag;
     }
-    long long spins = 0;
+    const unsigned long long t_give_up = __builtin_amdgcn_s_memrealtime() + kAgWaitTicks;
     for (;;) {
       bool all = true;
 #pragma unroll
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(kAgThreads) void k_allgather_granules(AllGatherPara
         }
       }
       if (all) break;
-      if (++spins > (1LL << 22)) {
+      if (__builtin_amdgcn_s_memrealtime() > t_give_up) {
         __hip_atomic_store(p.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

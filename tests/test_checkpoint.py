@@ -208,3 +208,28 @@ def test_oracle_built_checkpoint_loaded_on_gpu_matches_oracle(tmp_path, orc, qt)
         Yref = X.reshape(-1, K).double().numpy() @ orc.dequantize(o).astype(np.float16).astype(np.float64).T
         Y = lin(X.cuda()).double().cpu().numpy().reshape(-1, M)
         assert np.linalg.norm(Y - Yref) / np.linalg.norm(Yref) <= 1e-3
+
+
+def test_linear4bit_deepcopy_keeps_the_4bit_state():
+    """copy.deepcopy of a quantised Linear4bit (e.g. to keep an unsharded reference) keeps its
+    packed bytes and QuantState -- equal values, separate tensors -- and the copy's
+    Params4bit.module points to the copied module (torch's default Parameter.__deepcopy__
+    would drop the state)."""
+    import copy
+
+    from quantizations_amd.modules import Linear4bit
+
+    M, K = 128, 256
+    packed, qs = _oracle_state(M, K, "nf4", True, seed=7)
+    lin = Linear4bit(K, M, bias=False, quant_type="nf4", device="meta")
+    from quantizations_amd.core import Params4bit
+    lin.weight = Params4bit.from_prequantized(packed.reshape(-1, 1), qs.as_dict(packed=True), device="cpu", module=lin)
+    twin = copy.deepcopy(lin)
+    w, w2 = lin.weight, twin.weight
+    assert isinstance(w2, Params4bit) and w2.bnb_quantized and w2.quant_state is not None
+    assert w2.module is twin and twin.quant_state is w2.quant_state
+    assert torch.equal(w2.data, w.data) and w2.data.data_ptr() != w.data.data_ptr()
+    for a, b in ((w.quant_state.absmax, w2.quant_state.absmax), (w.quant_state.state2.absmax, w2.quant_state.state2.absmax),
+                 (w.quant_state.offset, w2.quant_state.offset), (w.quant_state.code, w2.quant_state.code)):
+        assert torch.equal(a, b) and a.data_ptr() != b.data_ptr()
+    assert w2.quant_state.shape == w.quant_state.shape and w2.quant_state.quant_type == "nf4"

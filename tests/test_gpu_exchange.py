@@ -82,9 +82,14 @@ def test_oneshot_allgather_two_processes_one_gpu():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
     for rank, bad, failed, epoch in res:
         assert not failed, f"rank {rank}: a peer's signal timed out"

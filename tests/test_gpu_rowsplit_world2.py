@@ -1,0 +1,116 @@
+"""GPU: the north-star multi-GPU layout at world size 2 on the real kernels -- every
+Linear4bit of a small Llama row-split over two ranks (RowShardedLinear4bit slicing the global
+quant state, block_base addressing, grouped q/k/v and gate/up shard launches) and the shards
+exchanged by the one-shot all-gather (exchange.OneShotAllGather, both protocols by payload),
+driven by bench.py's own decode loop (HIP-graph capture).  The box has one MI355X, so the two
+ranks are two processes on it mapping each other's exchange buffers (gloo only for the setup
+and barriers; RCCL cannot put two ranks on one GPU).  Each rank's logits of a teacher-forced
+prefill + decode step match the unsharded model's within fp16 rounding, and both ranks'
+greedy decodes agree with each other token for token."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+from test_distributed import _free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev):
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import replace_with_bnb_linear
+
+    cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=4, vocab_size=1024, max_position_embeddings=256)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).half().to(dev).eval()
+    replace_with_bnb_linear(model, quant_type="nf4", compute_dtype=torch.float32)
+    return cfg, model
+
+
+def _worker(rank, world, port, q):
+    try:
+        _work(rank, world, port, q)
+    except BaseException as e:  # report instead of leaving the peer blocked in a collective
+        q.put((rank, "error", f"{type(e).__name__}: {e}"))
+        raise
+
+
+def _work(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        import bench
+        from quantizations_amd.exchange import OneShotAllGather
+        from quantizations_amd.integration import fuse_projection_groups
+        from quantizations_amd.parallel import RowShardedLinear4bit, shard_model_linear4bit
+
+        dev = torch.device("cuda", 0)
+        cfg, model = _model(dev)
+        ref = copy.deepcopy(model)
+        ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
+        shard_model_linear4bit(model, rank, world, gatherer=ag)
+        n_groups = fuse_projection_groups(model)
+        fuse_projection_groups(ref)
+        ids = torch.randint(0, cfg.vocab_size, (1, 12), generator=torch.Generator().manual_seed(5)).to(dev)
+        with torch.inference_mode():
+            a = model(input_ids=ids).logits.float()          # prefill: multi-token shard launches
+            b = ref(input_ids=ids).logits.float()
+            prefill_rel = ((a - b).norm() / b.norm()).item()
+            a1 = model(input_ids=ids[:, :1]).logits.float()  # one token: grouped decode GEMVs
+            b1 = ref(input_ids=ids[:, :1]).logits.float()
+            decode_rel = ((a1 - b1).norm() / b1.norm()).item()
+        torch.cuda.synchronize()
+        dist.barrier()
+        # bench.py's decode loop, HIP-graph captured, at world 2
+        _, hist = bench.decode_bench_graph(model, cfg, steps=6, warmup=2, prompt_len=8, world=world, batch=1)
+        hist = hist.cpu()
+        allh = [None] * world
+        dist.all_gather_object(allh, hist)
+        q0 = model.model.layers[0].self_attn.q_proj
+        q.put((rank, n_groups, prefill_rel, decode_rel, bool(torch.equal(allh[0], allh[1])),
+               int((hist[:, 8:16] != 0).sum()), ag.failed(), isinstance(q0, RowShardedLinear4bit),
+               q0.r1 - q0.r0, q0.r0))
+        dist.barrier()
+        ag.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rowsplit_world2_oneshot_on_gpu():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
+        os.environ.get("PYTHONPATH", "")
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in res:
+        assert r[1] != "error", f"rank {r[0]}: {r[2]}"
+    for p in procs:
+        assert p.exitcode == 0
+    for rank, n_groups, prefill_rel, decode_rel, same, n_tok, failed, sharded, rows, r0 in res:
+        assert sharded and rows == 256 and n_groups == 4, (rank, rows, n_groups)
+        assert r0 == 256 * rank                      # q_proj rows [256 rank, +256) of 512
+        assert not failed, f"rank {rank}: an exchange timed out"
+        # row shards multiply the global state's exact weights; fp32 summation order and the
+        # fp16 rounding of a shard launch's outputs are the only differences
+        assert prefill_rel < 2e-3 and decode_rel < 2e-3, (rank, prefill_rel, decode_rel)
+        assert same, "the two ranks decoded different tokens"
+        assert n_tok > 0

@@ -188,7 +188,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
     if sharded:
         if tp_mode == "pair":
             from quantizations_amd.parallel import apply_tensor_parallel
-            apply_tensor_parallel(model, rank, world, local_matmul=local_matmul)
+            apply_tensor_parallel(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
         else:
             from quantizations_amd.parallel import shard_model_linear4bit
             shard_model_linear4bit(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
@@ -946,8 +946,7 @@ def main():
                                  dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16,
                                  compute_dtype=cdt)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
-                                                     layer_ops=layer_ops,
-                                                     gatherer=gatherer if tp_mode == "gather" else None)
+                                                     layer_ops=layer_ops, gatherer=gatherer)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"

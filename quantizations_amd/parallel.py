@@ -251,8 +251,9 @@ class RowParallelLinear4bit(nn.Module):
     rank's partial (not by P extra fp16 roundings inside the collective)."""
 
     def __init__(self, full: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 group=None, local_matmul: Optional[Callable] = None):
+                 group=None, local_matmul: Optional[Callable] = None, gatherer=None):
         super().__init__()
+        self.gatherer = gatherer  # None: dist.all_reduce; else the partials are all-gathered and summed
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world_size = dist.get_world_size(group) if world_size is None else world_size
         self.group = group
@@ -281,7 +282,14 @@ class RowParallelLinear4bit(nn.Module):
             else:
                 y = gemm_4bit(x_local, self.packed, self.state, bias=self.bias)
         y32 = y.float().contiguous()   # [..., M] fp32: 16 KiB at bs=1 for M = 4096
-        dist.all_reduce(y32, group=self.group)
+        if self.gatherer is not None and self.gatherer.accepts(y32):
+            # one-shot: every rank's fp32 partial lands here, summed in rank order (the same
+            # order on every rank, so all ranks hold identical sums)
+            parts = torch.empty((self.world_size,) + tuple(y32.shape), dtype=torch.float32, device=y32.device)
+            self.gatherer(parts, y32)
+            y32 = parts.sum(0)
+        else:
+            dist.all_reduce(y32, group=self.group)
         return y32.to(y.dtype)
 
 
@@ -290,7 +298,7 @@ TP_BLOCKS = ((("q_proj", "k_proj", "v_proj"), "o_proj"), (("gate_proj", "up_proj
 
 
 def apply_tensor_parallel(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None,
-                          group=None, local_matmul: Optional[Callable] = None) -> int:
+                          group=None, local_matmul: Optional[Callable] = None, gatherer=None) -> int:
     """Megatron-style TP pairing over the Linear4bit layers of a decoder
     (SURVEY.md 8f row 3): q/k/v and gate/up become column-parallel (each rank
     keeps its attention heads / MLP columns, no collective), o_proj and
@@ -316,7 +324,8 @@ def apply_tensor_parallel(model: nn.Module, rank: Optional[int] = None, world_si
             for nm in cols:
                 parent._modules[nm] = RowShardedLinear4bit(parent._modules[nm], rank, world, group, local_matmul,
                                                            gather=False)
-            parent._modules[row] = RowParallelLinear4bit(parent._modules[row], rank, world, group, local_matmul)
+            parent._modules[row] = RowParallelLinear4bit(parent._modules[row], rank, world, group, local_matmul,
+                                                         gatherer=gatherer)
             n += 1
     return n
 

@@ -233,7 +233,7 @@ def _tiny_llama_4bit():
     return cfg, model, ref
 
 
-def _tp_worker(rank, world, port, q, batch=1):
+def _tp_worker(rank, world, port, q, batch=1, oneshot=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -241,7 +241,11 @@ def _tp_worker(rank, world, port, q, batch=1):
         from quantizations_amd.parallel import RowParallelLinear4bit, apply_tensor_parallel
 
         cfg, model, ref = _tiny_llama_4bit()
-        n = apply_tensor_parallel(model, rank, world, local_matmul=_tp_hook)
+        ag = None
+        if oneshot:  # the row-parallel all-reduce as a one-shot gather of the fp32 partials + sum
+            from exchange_emulation import ShmAllGather
+            ag = ShmAllGather(slot_bytes=8192, tag=f"tp{port}")
+        n = apply_tensor_parallel(model, rank, world, local_matmul=_tp_hook, gatherer=ag)
         groups = fuse_projection_groups(model)
         ids = torch.tensor([[5, 17, 3, 88, 41, 9], [7, 2, 60, 11, 4, 30]])[:batch]
         with torch.no_grad():
@@ -264,25 +268,30 @@ def _tp_worker(rank, world, port, q, batch=1):
         rel_step = max(float((step - ref_step).norm() / ref_step.norm()),
                        float((st_step - ref_step).norm() / ref_step.norm()))
         o_proj = model.model.layers[0].self_attn.o_proj
+        if ag is not None:
+            assert ag.calls >= 4, ag.calls   # o and down of 2 layers went through it at least once
+            ag.close()
         q.put((rank, n, groups, rel, rel_step, isinstance(o_proj, RowParallelLinear4bit),
                model.model.layers[0].self_attn.q_proj.packed.numel()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("batch", [1, 2])
-def test_tensor_parallel_pairing_tiny_llama(batch):
+@pytest.mark.parametrize("batch,oneshot", [(1, False), (2, False), (2, True)])
+def test_tensor_parallel_pairing_tiny_llama(batch, oneshot):
     """Megatron TP pairing (column q/k/v/gate/up, row o/down + all-reduce) on a
     tiny Llama over gloo world 2: logits of prefill and of a cached decode step
     equal the unsharded model's (fp32 sums in another order).  batch 2 is the
-    bench's weak-scaling layout (one decode stream per GPU, TP over all GPUs)."""
+    bench's weak-scaling layout (one decode stream per GPU, TP over all GPUs); with
+    `oneshot` the row-parallel all-reduce runs as the one-shot exchange's gather of the
+    fp32 partials + a rank-ordered sum (the protocol rehearsed over shared memory)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
         os.environ.get("PYTHONPATH", "")
-    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, batch)) for r in range(world)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, batch, oneshot)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]

@@ -6,7 +6,9 @@ driven by bench.py's own decode loop (HIP-graph capture).  The box has one MI355
 ranks are two processes on it mapping each other's exchange buffers (gloo only for the setup
 and barriers; RCCL cannot put two ranks on one GPU).  Each rank's logits of a teacher-forced
 prefill + decode step match the unsharded model's within fp16 rounding, and both ranks'
-greedy decodes agree with each other token for token."""
+greedy decodes agree with each other token for token.  The same for the Megatron pairing
+(column-parallel q/k/v/gate/up on the local heads, row-parallel o/down whose fp32 partials the
+one-shot exchange gathers and every rank sums in rank order)."""
 import copy
 import os
 
@@ -34,15 +36,15 @@ def _model(dev):
     return cfg, model
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, layout):
     try:
-        _work(rank, world, port, q)
+        _work(rank, world, port, q, layout)
     except BaseException as e:  # report instead of leaving the peer blocked in a collective
         q.put((rank, "error", f"{type(e).__name__}: {e}"))
         raise
 
 
-def _work(rank, world, port, q):
+def _work(rank, world, port, q, layout):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
@@ -50,13 +52,16 @@ def _work(rank, world, port, q):
         import bench
         from quantizations_amd.exchange import OneShotAllGather
         from quantizations_amd.integration import fuse_projection_groups
-        from quantizations_amd.parallel import RowShardedLinear4bit, shard_model_linear4bit
+        from quantizations_amd.parallel import RowShardedLinear4bit, apply_tensor_parallel, shard_model_linear4bit
 
         dev = torch.device("cuda", 0)
         cfg, model = _model(dev)
         ref = copy.deepcopy(model)
         ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
-        shard_model_linear4bit(model, rank, world, gatherer=ag)
+        if layout == "gather":
+            shard_model_linear4bit(model, rank, world, gatherer=ag)
+        else:   # Megatron pairing: column q/k/v/gate/up, row o/down with the one-shot all-reduce
+            apply_tensor_parallel(model, rank, world, gatherer=ag)
         n_groups = fuse_projection_groups(model)
         fuse_projection_groups(ref)
         ids = torch.randint(0, cfg.vocab_size, (1, 12), generator=torch.Generator().manual_seed(5)).to(dev)
@@ -84,14 +89,15 @@ def _work(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_rowsplit_world2_oneshot_on_gpu():
+@pytest.mark.parametrize("layout", ["gather", "pair"])
+def test_rowsplit_world2_oneshot_on_gpu(layout):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
         os.environ.get("PYTHONPATH", "")
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, layout)) for r in range(world)]
     for p in procs:
         p.start()
     try:

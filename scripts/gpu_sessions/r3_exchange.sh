@@ -13,6 +13,6 @@ step() {  # name timeout cmd...
   echo "== $name rc=$rc"; tail -4 "gpurun_out/$name.log" | cut -c1-600
   [ $rc -eq 0 ] || exit $rc
 }
-step r3d_exchange 300 python -u -m pytest tests/test_gpu_exchange.py -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider
+step r3d_exchange 300 python -u -m pytest tests/test_gpu_xgmi_exchange.py -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider
 step r3d_tp1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 1 --force-shard --steps 32 --warmup 4 --no-prefill --no-cpu --no-extra-weak
 step r3d_pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider

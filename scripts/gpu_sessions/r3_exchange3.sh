@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_exchange.py -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r3j_exchange.log 2>&1 || { tail -40 gpurun_out/r3j_exchange.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_xgmi_exchange.py -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/r3j_exchange.log 2>&1 || { tail -40 gpurun_out/r3j_exchange.log; exit 1; }
 tail -1 gpurun_out/r3j_exchange.log
 timeout -k 10 300 python scripts/exchange_times.py --world 1 > gpurun_out/r3j_times_w1.log 2>&1 || { tail -30 gpurun_out/r3j_times_w1.log; exit 1; }
 grep '^{' gpurun_out/r3j_times_w1.log

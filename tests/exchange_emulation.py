@@ -5,7 +5,7 @@ rank and pulls rank b's granules once tagged) for payloads up to 2 KiB, plain sl
 [parity][rank] + epoch flags (k_allgather_flags) above, epoch parity -- run by each gloo rank over
 shared-memory files standing in for the IPC-mapped device buffers.  Used by
 tests/test_exchange.py to check shard placement, ordering and the parity double buffer on
-CPU; the device protocol itself runs in tests/test_gpu_exchange.py."""
+CPU; the device protocol itself runs in tests/test_gpu_xgmi_exchange.py."""
 from __future__ import annotations
 
 import os

@@ -1206,6 +1206,443 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_gemm16_4d: the 4-wave 256 x 256 tile (each wave a 128-token x 128-row quadrant, the 256
+// accumulator registers in AGPRs) staged ONLY by LDS DMA, two steps ahead with two buffers.
+//
+// A wave holds a whole step's fragments in registers (X and W, both k-halves: 128 VGPRs), so a
+// buffer is free for the next DMA as soon as every wave has read it -- not when its MFMAs are
+// done.  Step s (buffer b = s & 1) is three segments:
+//   A: k-half 0 MFMAs of rows 0-3 (32) with the 16 ds_read_b128 of k-half 1 from buffer b;
+//      lgkmcnt(0) + s_barrier: every wave has buffer b in registers
+//   B: k-half 0 MFMAs of rows 4-7 (32) with the 16 DMAs of step s + 2 into buffer b;
+//      vmcnt(16) (this wave's step s + 1 DMAs, issued one step earlier, have landed) + s_barrier
+//   C: k-half 1 MFMAs (64) with the 16 ds_read_b128 of step s + 1's k-half 0 from buffer b ^ 1
+// so a DMA has ~1.5 steps of MFMAs to land, nothing but the staging bytes goes through LDS,
+// and the loop carries no VALU address arithmetic: the DMAs are buffer loads whose per-lane
+// part (row, swizzled chunk) is a fixed VGPR and whose k offset is a scalar (soffset).
+// Rows past T or M are clamped (their outputs are not stored); the LDS image and fragment
+// addresses are those of k_gemm16_4w (16-B chunk XOR swizzle applied to the DMA source).
+// compile-time loop: f(std::integral_constant<int, 0>{}) .. f(<N - 1>) (a 128-iteration body
+// is past the unroller's budget for #pragma unroll, and every index below must be a constant)
+template <typename F, int... Ns>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, Ns...>) {
+  (f(std::integral_constant<int, Ns>{}), ...);
+}
+template <int N, typename F> __device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+constexpr int k4dBuf = 2 * k4wStage;  // X image + W image of one step
+constexpr int k4dLds = (2 * k4dBuf > 4 * 128 * k4wERow) ? 2 * k4dBuf : 4 * 128 * k4wERow;
+template <int DT, int SK = 0, int P1 = 32, int P2 = 96>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4d(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[k4dLds];
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 1, wm = wave & 1;
+
+  // XCD-aware, bijective tile order (as k_gemm_4bit_big)
+  const int tiles_m = (p.M + k4wM - 1) / k4wM;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int tm = wg % tiles_m, tt = wg / tiles_m;
+  if constexpr ((SK & 64) != 0) {
+    // grouped order: the 32 tiles an XCD runs together cover 4 token tiles x 8 row tiles
+    const int tiles_t = (p.T + k4wT - 1) / k4wT;
+    if (tiles_m % 8 == 0 && tiles_t % 4 == 0) {
+      const int grp = wg / (4 * tiles_m), r = wg % (4 * tiles_m);
+      tt = 4 * grp + (r % 32) / 8;
+      tm = 8 * (r / 32) + r % 8;
+    }
+  }
+  const int m0 = tm * k4wM, t0 = tt * k4wT;
+  const int nsteps = p.K / kBK;
+
+  // DMA c (0..7) of a thread moves 16-B chunk (tid & 7) of rows 32 c + tid / 8 of X and of W;
+  // wave w's instruction c fills LDS rows 32 c + 8 w .. + 7 (1 KiB, lane-linear)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(p.X), (short)0, (int)((uint32_t)p.T * (uint32_t)p.ldx * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char *>(p.B), (short)0, (int)((uint32_t)p.M * (uint32_t)p.K * 2u), 0x00020000);
+  const uint32_t sw = (uint32_t)((tid & 7) ^ ((tid >> 4) & 7));
+  uint32_t xo[8], wo[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int row = 32 * c + (tid >> 3);
+    xo[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * sw) * 2u;
+    wo[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sw) * 2u;
+  }
+  // h = 0: X rows, h = 1: W rows
+  auto dma_half = [&](int step, int buf, int c, int h) {
+    const int kb = (SK & 4) ? 0 : step * (kBK * 2);
+    unsigned char *d = smem + buf * k4dBuf + 4096 * c + 1024 * wave;
+    if (h == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)d, 16, xo[c], kb, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(d + k4wStage), 16, wo[c], kb, 0, 0);
+  };
+  auto dma = [&](int step, int buf, int c) {
+    dma_half(step, buf, c, 0);
+    dma_half(step, buf, c, 1);
+  };
+
+  // fragments: lane (fr, fk) of a 16 x 32 operand holds row fr, k 8 fk .. +8 of the k-half
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                          (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  v4u xf[2][8], wf[2][8];
+  // SK & 32: v_mfma_f32_32x32x16 (64 MFMAs of 32 cycles per step instead of 128 of 16: half the
+  // MFMA issue holds, more issue room for the DMAs and reads).  A/B lane (r32, h32) holds row
+  // r32, k = 8 h32 .. +8 of k16 slice 2 kk + q (chunk 2 (2 kk + q) + h32, same swizzle); the 8
+  // fragments of a k-half per operand are [q][tile].  D: lane holds token r32 of its 32-token
+  // tile, rows 8 g + 4 h32 + r (register 4 g + r).
+  constexpr bool kM32 = (SK & 32) != 0;
+  constexpr int kNM = kM32 ? 64 : 128;  // MFMAs per step
+  typedef float f16v_t __attribute__((ext_vector_type(16)));
+  const int r32 = lane & 31, h32 = lane >> 5;
+  uint32_t fl32[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) fl32[q] = (uint32_t)(r32 * 128 + (((2 * q + h32) ^ ((r32 >> 1) & 7)) << 4));
+  // read g of a k-half, in the order the MFMAs consume them.  16x16x32: W fragment 0, the 8 X
+  // fragments (tokens 16 i ..), W fragments 1-7.  32x32x16, per k16 slice q (8 reads): W tile 0,
+  // X tiles 0-3, W tiles 1-3 -> stored as xf[kk][4 q + i], wf[kk][4 q + j]
+  auto frag_read = [&](int buf, int kk, int g) {
+    const unsigned char *bs = smem + buf * k4dBuf;
+    if constexpr (kM32) {
+      const int q = g >> 3, h = g & 7;
+      const uint32_t o = fl32[2 * kk + q];
+      if (h >= 1 && h <= 4)
+        xf[kk][4 * q + h - 1] = *reinterpret_cast<const v4u *>(bs + (128 * wt + 32 * (h - 1)) * 128 + o);
+      else {
+        const int j = h == 0 ? 0 : h - 4;
+        wf[kk][4 * q + j] = *reinterpret_cast<const v4u *>(bs + k4wStage + (128 * wm + 32 * j) * 128 + o);
+      }
+      return;
+    }
+    const unsigned char *bx = bs + fl[kk];
+    const int wj = g == 0 ? 0 : g - 8;
+    if (g >= 1 && g <= 8) xf[kk][g - 1] = *reinterpret_cast<const v4u *>(bx + (128 * wt + 16 * (g - 1)) * 128);
+    else wf[kk][wj] = *reinterpret_cast<const v4u *>(bx + k4wStage + (128 * wm + 16 * wj) * 128);
+  };
+  f4_t acc[kM32 ? 1 : 8][kM32 ? 1 : 8];
+  f16v_t acc32[kM32 ? 4 : 1][kM32 ? 4 : 1];
+  if constexpr (kM32) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[j][i][e] = 0.0f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // MFMA n of k-half kk.  16x16x32 (n < 64): row fragment j = n / 8, token fragment i = n % 8.
+  // 32x32x16 (n < 32): slice q = n / 16, row tile j = (n / 4) % 4, token tile i = n % 4.
+  // SK & 16: as inline asm with the accumulator tied to one AGPR quad ("+a").
+  auto mfma = [&](int kk, int n) {
+    if constexpr (kM32) {
+      const int q = n >> 4, j = (n >> 2) & 3, i = n & 3;
+      if constexpr (DT == QZ_DT_F16)
+        acc32[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, wf[kk][4 * q + j]),
+                                                             __builtin_bit_cast(h8_t, xf[kk][4 * q + i]), acc32[j][i],
+                                                             0, 0, 0);
+      else
+        acc32[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8_t, wf[kk][4 * q + j]),
+                                                              __builtin_bit_cast(b8_t, xf[kk][4 * q + i]),
+                                                              acc32[j][i], 0, 0, 0);
+      return;
+    }
+    const int j = n >> 3, i = n & 7;
+    if constexpr ((SK & 16) != 0) {
+      if constexpr (DT == QZ_DT_F16)
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[j][i]) : "v"(wf[kk][j]), "v"(xf[kk][i]));
+      else
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j][i]) : "v"(wf[kk][j]), "v"(xf[kk][i]));
+    } else if constexpr (DT == QZ_DT_F16) {
+      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, wf[kk][j]),
+                                                         __builtin_bit_cast(h8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+    } else {
+      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, wf[kk][j]),
+                                                          __builtin_bit_cast(b8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+    }
+  };
+  // ---- prologue: steps 0 and 1 in flight, step 0's k-half 0 in registers ----
+#pragma unroll
+  for (int c = 0; c < 8; ++c) dma(0, 0, c);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) dma(min(1, nsteps - 1), 1, c);
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int g = 0; g < 16; ++g) frag_read(0, 0, g);
+  if constexpr ((SK & 16) != 0) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+
+  // One loop body for every step (a peeled tail split the accumulators between AGPRs and
+  // VGPRs): the last two steps stage clamped copies of the last step into buffers nobody reads
+  // again, and the last step reads a k-half it does not use.  The kNM MFMAs of a step (k-half 0
+  // then 1) carry, pinned in program order by sched_barrier:
+  //   [0, P1)    the 16 k-half 1 fragment reads of buffer b;  lgkmcnt(0) + s_barrier
+  //   [P1, P2)   step s + 2's 16 DMAs into buffer b;  vmcnt(16) + s_barrier
+  //   [P2, kNM)  step s + 1's 16 k-half 0 fragment reads of buffer b ^ 1
+  // (P2 >= kNM / 2: the k-half 0 registers are free; every DMA has a whole step of MFMAs to land.)
+  static_assert(P1 % 16 == 0 && P1 > 0 && P1 <= kNM / 2 && (P2 - P1) % 16 == 0 && P2 > P1 && P2 >= kNM / 2 &&
+                P2 < kNM && (kNM - P2) % 16 == 0, "k_gemm16_4d segment bounds");
+  constexpr int kR1 = P1 / 16, kD = (P2 - P1) / 16, kR0 = (kNM - P2) / 16;
+  for (int s = 0; s < nsteps; ++s) {
+    const int b = s & 1;
+    const int s2 = min(s + 2, nsteps - 1);
+    static_for<kNM>([&](auto nc) {
+      constexpr int n = decltype(nc)::value;
+      mfma(n / (kNM / 2), n % (kNM / 2));
+      if constexpr (n < P1) {
+        if constexpr ((n + 1) % kR1 == 0) {
+          if constexpr ((SK & 2) == 0) frag_read(b, 1, (n + 1) / kR1 - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (n == P1 - 1) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if constexpr (n < P2) {
+        if constexpr ((n + 1 - P1) % kD == 0) {
+          constexpr int d = (n + 1 - P1) / kD - 1;
+          if constexpr ((SK & 1) == 0) dma_half(s2, b, d >> 1, d & 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (n == P2 - 1) {
+          __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if constexpr ((n + 1 - P2) % kR0 == 0) {
+        if constexpr ((SK & 2) == 0) frag_read(b ^ 1, 0, (n + 1 - P2) / kR0 - 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+  }
+  if constexpr ((SK & 16) != 0) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+
+  // ---- epilogue: quadrant -> LDS image [128 tokens][128 rows] (+ bias) -> coalesced rows ----
+  __syncthreads();
+  unsigned char *ew = smem + wave * (128 * k4wERow);
+  if constexpr (kM32) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = 32 * j + 8 * g + 4 * h32;
+        float bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[r] = p.bias ? load_f32<DT>(p.bias, min(m0 + 128 * wm + row + r, p.M - 1)) : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f16v_t &v = acc32[j][i];
+          const uint32_t l2 = cvt_pk16<DT>(v[4 * g] + bv[0], v[4 * g + 1] + bv[1]);
+          const uint32_t h2 = cvt_pk16<DT>(v[4 * g + 2] + bv[2], v[4 * g + 3] + bv[3]);
+          *reinterpret_cast<uint2 *>(ew + (32 * i + r32) * k4wERow + row * 2) = uint2{l2, h2};
+        }
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bv[r] = p.bias ? load_f32<DT>(p.bias, min(m0 + 128 * wm + 16 * j + 4 * fk + r, p.M - 1)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f4_t v = acc[j][i];
+        const uint32_t l2 = cvt_pk16<DT>(v[0] + bv[0], v[1] + bv[1]);
+        const uint32_t h2 = cvt_pk16<DT>(v[2] + bv[2], v[3] + bv[3]);
+        *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * k4wERow + (16 * j + 4 * fk) * 2) = uint2{l2, h2};
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int qd = lane + 64 * it, tok = qd >> 4, c16 = qd & 15;
+    const v4u v = *reinterpret_cast<const v4u *>(ew + tok * k4wERow + c16 * 16);
+    const int t = t0 + 128 * wt + tok, m = m0 + 128 * wm + 8 * c16;
+    if constexpr ((SK & 128) != 0) {  // timing only: no global stores (the image is still read)
+      if (v.x == 0x7FFF7FFFu && v.y == 0x12345678u) *reinterpret_cast<v4u *>(p.Y) = v;
+      continue;
+    }
+    if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_gemm16_4p: k_gemm16_4d's step (P1 = 16, P2 = 112, 16x16x32) in a persistent workgroup that
+// walks tiles id, id + grid, ... (grouped XCD-aware order).  The last two steps of a tile stage
+// the NEXT tile's steps 0 and 1, so its k-half 0 fragments are in registers when the tile ends,
+// and the epilogue stores straight from the accumulators (8-B stores: 16 tokens x 32 B per
+// instruction, merged in L2) without the LDS image -- no prologue wait, no epilogue barrier.
+struct Gemm4pOffs {
+  uint32_t x[8], w[8];
+};
+template <int DT, int SK = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4p(GemmParams p) {
+  constexpr int P1 = 16, P2 = 112;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * k4dBuf];
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 1, wm = wave & 1;
+  const int tiles_m = (p.M + k4wM - 1) / k4wM, tiles_t = (p.T + k4wT - 1) / k4wT;
+  const int ntiles = tiles_m * tiles_t;
+  const int nsteps = p.K / kBK;
+  // tile id -> (m0, t0): XCD-aware bijection, then the grouped order (4 token x 8 row tiles)
+  auto tile_of = [&](int id, int &m0, int &t0) {
+    const int q8 = ntiles >> 3, r8 = ntiles & 7, xcd = id & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+    int tm = wg % tiles_m, tt = wg / tiles_m;
+    if (tiles_m % 8 == 0 && tiles_t % 4 == 0) {
+      const int grp = wg / (4 * tiles_m), r = wg % (4 * tiles_m);
+      tt = 4 * grp + (r % 32) / 8;
+      tm = 8 * (r / 32) + r % 8;
+    }
+    m0 = tm * k4wM;
+    t0 = tt * k4wT;
+  };
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(p.X), (short)0, (int)((uint32_t)p.T * (uint32_t)p.ldx * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char *>(p.B), (short)0, (int)((uint32_t)p.M * (uint32_t)p.K * 2u), 0x00020000);
+  const uint32_t sw = (uint32_t)((tid & 7) ^ ((tid >> 4) & 7));
+  // per-lane DMA offsets of a tile (rows clamped into the tensors)
+  typedef Gemm4pOffs Offs;
+  auto offs_of = [&](int m0, int t0, Offs &o) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int row = 32 * c + (tid >> 3);
+      o.x[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * sw) * 2u;
+      o.w[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sw) * 2u;
+    }
+  };
+  auto dma_half = [&](const Offs &o, int step, int buf, int c, int h) {
+    const int kb = step * (kBK * 2);
+    unsigned char *d = smem + buf * k4dBuf + 4096 * c + 1024 * wave;
+    if (h == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)d, 16, o.x[c], kb, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(d + k4wStage), 16, o.w[c], kb, 0, 0);
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                          (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  v4u xf[2][8], wf[2][8];
+  auto frag_read = [&](int buf, int kk, int g) {
+    const unsigned char *bx = smem + buf * k4dBuf + fl[kk];
+    const int wj = g == 0 ? 0 : g - 8;
+    if (g >= 1 && g <= 8) xf[kk][g - 1] = *reinterpret_cast<const v4u *>(bx + (128 * wt + 16 * (g - 1)) * 128);
+    else wf[kk][wj] = *reinterpret_cast<const v4u *>(bx + k4wStage + (128 * wm + 16 * wj) * 128);
+  };
+  f4_t acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&](int kk, int n) {
+    const int j = n >> 3, i = n & 7;
+    if constexpr (DT == QZ_DT_F16)
+      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, wf[kk][j]),
+                                                         __builtin_bit_cast(h8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+    else
+      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, wf[kk][j]),
+                                                          __builtin_bit_cast(b8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
+  };
+
+  int id = blockIdx.x;
+  if (id >= ntiles) return;
+  int m0, t0, nm0 = 0, nt0 = 0;
+  tile_of(id, m0, t0);
+  Offs cur, nxt;
+  offs_of(m0, t0, cur);
+  // ---- first tile: steps 0 and 1 in flight, step 0's k-half 0 in registers ----
+#pragma unroll
+  for (int c = 0; c < 8; ++c) { dma_half(cur, 0, 0, c, 0); dma_half(cur, 0, 0, c, 1); }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) { dma_half(cur, min(1, nsteps - 1), 1, c, 0); dma_half(cur, min(1, nsteps - 1), 1, c, 1); }
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int g = 0; g < 16; ++g) frag_read(0, 0, g);
+
+  int gs = 0;  // global step: buffer parity across tiles
+  for (;;) {
+    const int nid = id + (int)gridDim.x;
+    const bool more = nid < ntiles;
+    if (more) {
+      tile_of(nid, nm0, nt0);
+      offs_of(nm0, nt0, nxt);
+    } else {
+      nxt = cur;
+    }
+    for (int s = 0; s < nsteps; ++s, ++gs) {
+      const int b = gs & 1;
+      // DMA source: step s + 2 of this tile, else step s + 2 - nsteps of the next (clamped
+      // copies of this tile's last step after the last tile)
+      const bool into_next = s + 2 >= nsteps;
+      const Offs &so = into_next ? nxt : cur;
+      const int s2 = into_next ? (more ? s + 2 - nsteps : nsteps - 1) : s + 2;
+      static_for<128>([&](auto nc) {
+        constexpr int n = decltype(nc)::value;
+        mfma(n >> 6, n & 63);
+        if constexpr (n < P1) {
+          frag_read(b, 1, n);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (n == P1 - 1) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else if constexpr (n < P2) {
+          if constexpr ((n + 1 - P1) % 6 == 0) {
+            constexpr int d = (n + 1 - P1) / 6 - 1;
+            dma_half(so, s2, b, d >> 1, d & 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (n == P2 - 1) {
+            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {
+          frag_read(b ^ 1, 0, n - P2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+    }
+    // ---- epilogue: accumulators (+ bias) -> Y, 8 B per lane per store; then zero them ----
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + 128 * wm + 16 * j + 4 * fk;
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = p.bias ? load_f32<DT>(p.bias, min(m + r, p.M - 1)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = t0 + 128 * wt + 16 * i + fr;
+        const f4_t v = acc[j][i];
+        const uint2 o = uint2{cvt_pk16<DT>(v[0] + bv[0], v[1] + bv[1]), cvt_pk16<DT>(v[2] + bv[2], v[3] + bv[3])};
+        if ((SK & 128) == 0 && t < p.T && m < p.M)
+          *reinterpret_cast<uint2 *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = o;
+        acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (!more) break;
+    id = nid;
+    m0 = nm0;
+    t0 = nt0;
+    cur = nxt;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+}
+
 // Multi-token GEMV for 2 <= T <= 16 (small-batch decode, short prefills).
 // A 512-thread workgroup owns 16 weight rows; its 8 waves split K and meet in
 // LDS (no workspace, no second launch).  Per 256-element chunk, lane
@@ -1435,9 +1872,9 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 
 extern "C" int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy);
 
-// Dense 16-bit GEMM on the staggered 8-phase schedule (k_gemm_4bit_8p<.., kPlainW>): the second
-// half of the large-T prefill route "dequantise once (qz_dequantize_4bit, bit-exact), then GEMM"
-// (modules.py:62-64's own structure, both halves hand-written for gfx950).
+// Dense 16-bit GEMM (k_gemm16_4d: 4 waves, 256 x 256 tile, LDS-DMA staging two steps ahead): the
+// second half of the large-T prefill route "dequantise once (qz_dequantize_4bit, bit-exact), then
+// GEMM" (modules.py:62-64's own structure, both halves hand-written for gfx950).
 extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dtype, const void *W, const void *bias,
                              void *Y, int ldy, void *stream) {
   if (!X || !W || !Y || T < 0 || M < 0 || K < 0) return QZ_ERR_ARG;
@@ -1455,12 +1892,12 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   p.ldx = ldx;
   p.ldy = ldy;
   p.k_split = K;
-  const unsigned g = (unsigned)(((M + kBigM - 1) / kBigM) * ((T + kBigT - 1) / kBigT));
+  const unsigned g = (unsigned)(((M + k4wM - 1) / k4wM) * ((T + k4wT - 1) / k4wT));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == QZ_DT_F16)
-    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, kPlainW, 1>), dim3(g), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_BF16, kPlainW, 1>), dim3(g), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_BF16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

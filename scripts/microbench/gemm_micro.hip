@@ -71,10 +71,16 @@ int main(int argc, char **argv) {
 #define P4W(SK_) vs.push_back({"4wave fp16 GEMM SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
       q.B = reinterpret_cast<const unsigned char *>(W16); const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
       hipLaunchKernelGGL((k_gemm16_4w<QZ_DT_F16, SK_>), dim3(g), dim3(256), 0, 0, q); }, {}})
+#define P4D(SK_, P1_, P2_) vs.push_back({"4wave-dma fp16 GEMM SK=" #SK_ " P=" #P1_ "," #P2_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
+      q.B = reinterpret_cast<const unsigned char *>(W16); const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
+      hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, SK_, P1_, P2_>), dim3(g), dim3(256), 0, 0, q); }, {}})
+#define P4P(SK_) vs.push_back({"4wave-persistent fp16 GEMM SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
+      q.B = reinterpret_cast<const unsigned char *>(W16); const unsigned g = (unsigned)std::min(((M + 255) / 256) * ((T + 255) / 256), 256); \
+      hipLaunchKernelGGL((k_gemm16_4p<QZ_DT_F16, SK_>), dim3(g), dim3(256), 0, 0, q); }, {}})
 #define P8S(SK_) vs.push_back({"8phase V=0 SK=" #SK_ " T=" + std::to_string(T), T, [=]() { GemmParams q = p; q.T = T; \
         const unsigned g = (unsigned)(((M + 255) / 256) * ((T + 255) / 256)); \
         hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, SK_>), dim3(g), dim3(512), 0, 0, q); }, {}})
-    if (T >= 4096) { PLV(1); PLV(257); }
+    if (T >= 4096) { PLV(1); P4D(64, 16, 112); P4P(0); P4P(128); }
   }
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());
@@ -99,7 +105,7 @@ int main(int argc, char **argv) {
       if (plain) { a.B = b2.B = reinterpret_cast<const unsigned char *>(W16); }
       if (plain) {
         hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, 5, 1>), dim3(g), dim3(512), 0, 0, a);
-        hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, false, QZ_DT_F16, 5, 257>), dim3(g), dim3(512), 0, 0, b2);
+        hipLaunchKernelGGL((k_gemm16_4p<QZ_DT_F16, 0>), dim3(std::min(g, 256u)), dim3(256), 0, 0, b2);
       } else {
         hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, 1>), dim3(g), dim3(512), 0, 0, a);
         hipLaunchKernelGGL((k_gemm_4bit_8p<QZ_NF4, true, QZ_DT_F16, 0, 65>), dim3(g), dim3(512), 0, 0, b2);
@@ -114,7 +120,7 @@ int main(int argc, char **argv) {
         maxd = std::max(maxd, (double)std::fabs(a1 - a2)); maxv = std::max(maxv, (double)std::fabs(a1));
         ndiff += h1[i] != h2[i];
       }
-      printf("check %s: SK257(plain)/SK65(fused) vs 8phase SK1 max|diff| %.4g (max|y| %.4g), %zu of %zu elements differ\n", plain ? "plain" : "fused",
+      printf("check %s: 4wave-persistent(plain)/SK65(fused) vs 8phase SK1 max|diff| %.4g (max|y| %.4g), %zu of %zu elements differ\n", plain ? "plain" : "fused",
              maxd, maxv, ndiff, h1.size());
     }
   }

@@ -2,7 +2,7 @@
 (bit-exact, ours) + qz_gemm_16bit (8-phase MFMA, ours) route vs dequant + the
 library GEMM (hipBLASLt, the reference's F.linear), plus the fused kernel; and a
 rel-err check of qz_gemm_16bit against an fp64 product.  Sets GEMM16_MIN_TILES.
-   python scripts/prefill_route_sweep.py"""
+   python scripts/prefill_route_sweep.py [T,T,...]   (default 513,1024,2048,4096,8192,16384)"""
 import json
 import os
 import sys
@@ -27,12 +27,13 @@ def timed(fn, iters=10):
 
 
 dev = torch.device("cuda")
+Ts = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else [513, 1024, 2048, 4096, 8192, 16384]
 out = {}
 for (M, K) in [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)]:
     torch.manual_seed(M + K)
     packed, st = quantize_4bit((torch.randn(M, K, device=dev) * 0.02).half(), quant_type="nf4")
     W = dequantize_4bit(packed, st).t()
-    for T in (513, 1024, 2048, 4096, 8192, 16384):
+    for T in Ts:
         x = torch.randn(T, K, device=dev, dtype=torch.float16)
         ref = (x.double() @ W.double().t())
         y = gemm_16bit(x, W)

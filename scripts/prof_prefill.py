@@ -1,6 +1,7 @@
 """Both prefill routes at config #4 (T = 8 x 2048 = 16384 tokens, 4096x4096 NF4+DQ) for
 rocprofv3 passes: the fused MFMA kernel, then dequantize_4bit + hipBLASLt.
-   python scripts/prof_prefill.py [iters]"""
+   python scripts/prof_prefill.py [iters] [route,route,...]   (default fused,dequant; gemm16 = dequant +
+   our 16-bit GEMM)"""
 import os
 import sys
 
@@ -14,7 +15,8 @@ dev = torch.device("cuda")
 torch.manual_seed(0)
 packed, st = quantize_4bit((torch.randn(4096, 4096, device=dev) * 0.02).half(), quant_type="nf4")
 x = torch.randn(16384, 4096, device=dev, dtype=torch.float16)
-for route in ("fused", "dequant"):
+routes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fused", "dequant"]
+for route in routes:
     for _ in range(iters):
         gemm_4bit(x, packed, st, route=route)
     torch.cuda.synchronize()

@@ -598,7 +598,7 @@ def prefill_bench(T: int = 16384, iters: int = 10):
             return torch.nn.functional.linear(x, dequantize_4bit(packed, qs).t())
 
         res = {}
-        for name, fn in (("fused", fused), ("dequant+gemm16_8phase", own_route), ("dequant+hipblaslt", ref_route)):
+        for name, fn in (("fused", fused), ("dequant+gemm16", own_route), ("dequant+hipblaslt", ref_route)):
             fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -614,11 +614,11 @@ def prefill_bench(T: int = 16384, iters: int = 10):
     from quantizations_amd.core import GEMM16_MIN_TILES, PREFILL_GEMM16, fused_max_tokens
     return {"tokens": T, "shapes": out, "mfma_peak_TFLOPs_f16_dense": 2500.0,
             "product_route": "fused" if T <= fused_max_tokens(4096) else
-                             ("dequant+gemm16_8phase" if PREFILL_GEMM16 else "dequant+hipblaslt"),
+                             ("dequant+gemm16" if PREFILL_GEMM16 else "dequant+hipblaslt"),
             "note": "every route multiplies the same bit-exact dequantised weight; matmul_4bit takes the fused "
                     f"MFMA kernels up to {fused_max_tokens(4096)} tokens ({fused_max_tokens(1024)} for 1024 or "
                     f"14336 rows), above it our dequant kernel + hipBLASLt "
-                    "(the reference's F.linear route) unless QZ_PREFILL_GEMM16=1 selects our 8-phase MFMA GEMM "
+                    "(the reference's F.linear route) unless QZ_PREFILL_GEMM16=1 selects our 4-wave LDS-DMA MFMA GEMM "
                     f"(qz_gemm_16bit, >= {GEMM16_MIN_TILES} 256x256 tiles)"}
 
 

@@ -486,11 +486,11 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
 # reference's own route (modules.py:62-64) -- full-weight dequantize_4bit (our
 # bit-exact HIP kernel) then the library GEMM (hipBLASLt), or, with
 # PREFILL_GEMM16 (env QZ_PREFILL_GEMM16=1) and >= GEMM16_MIN_TILES 256 x 256
-# output tiles, our staggered 8-phase MFMA GEMM (qz_gemm_16bit); "gemm16"
+# output tiles, our 4-wave LDS-DMA MFMA GEMM (qz_gemm_16bit); "gemm16"
 # forces the latter where it applies.  "auto" takes the fused kernel up to
 # fused_max_tokens(M) tokens and the dequant route above it (DESIGN.md
-# section 4.2 has the measured crossovers: hipBLASLt is 12-17 % faster than
-# qz_gemm_16bit at T >= 4096 today, so it stays the default).
+# section 4.2 has the measured crossovers: hipBLASLt is 4-7 % faster than
+# qz_gemm_16bit at T = 16384 today, so it stays the default).
 _FUSED_MAX_T_ENV = os.environ.get("QZ_PREFILL_FUSED_MAX_T")
 PREFILL_FUSED_MAX_TOKENS = int(_FUSED_MAX_T_ENV) if _FUSED_MAX_T_ENV else None   # None = the measured table
 PREFILL_GEMM16 = os.environ.get("QZ_PREFILL_GEMM16", "0") == "1"

@@ -179,12 +179,15 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 
 
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
-                         fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None):
+                         fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
+                         prenorm: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
-    groups and the one-launch layer ops.  `local_matmul` is the CPU test hook of
-    parallel.py (None = the HIP kernels).  Returns (n_groups, n_layer_ops)."""
+    groups and the one-launch layer ops, and (single-GPU layout, `prenorm`) absorb
+    each layer's two RMSNorms into those groups' launches.  `local_matmul` is the CPU
+    test hook of parallel.py (None = the HIP kernels).  Returns (n_groups,
+    n_layer_ops); absorbed norms count as layer ops."""
     if sharded:
         if tp_mode == "pair":
             from quantizations_amd.parallel import apply_tensor_parallel
@@ -207,6 +210,9 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      rope=layer_ops in ("all", "all+decoder", "rope"),
                                      mlp=layer_ops in ("all", "all+decoder", "mlp"),
                                      decoder=layer_ops == "all+decoder")  # one HIP launch each
+    if prenorm and fuse and not sharded and layer_ops in ("all", "norm"):
+        from quantizations_amd.integration import fuse_prenorm
+        n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
     return n_groups, n_layer_ops
 
 
@@ -854,6 +860,9 @@ def main():
     ap.add_argument("--no-fuse", action="store_true", help="one GEMV launch per Linear4bit (no q/k/v, gate/up groups)")
     ap.add_argument("--no-layer-ops", action="store_true",
                     help="keep transformers' eager RMSNorm / rotary (8 and 10 launches) instead of layer_ops")
+    ap.add_argument("--no-prenorm", action="store_true",
+                    help="keep each RMSNorm as its own launch (default: absorbed into the q/k/v and gate/up "
+                         "grouped GEMV launches on one GPU)")
     ap.add_argument("--layer-ops", choices=("all", "all+decoder", "norm", "rope", "mlp", "none"), default="all",
                     help="which transformers ops integration.fuse_layer_ops replaces")
     ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
@@ -946,7 +955,8 @@ def main():
                                  dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float16,
                                  compute_dtype=cdt)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
-                                                     layer_ops=layer_ops, gatherer=gatherer)
+                                                     layer_ops=layer_ops, gatherer=gatherer,
+                                                     prenorm=not args.no_prenorm)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1068,6 +1078,8 @@ def main():
             "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         line["config"]["compute_dtype"] = args.compute_dtype
+        line["config"]["rmsnorm_in_grouped_gemv"] = bool(not args.no_prenorm and not sharded and not args.no_fuse
+                                                         and layer_ops in ("all", "norm"))
         if exchange is not None:
             line["config"]["exchange"] = exchange
         if extra_codes is not None:

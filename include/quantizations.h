@@ -142,6 +142,18 @@ typedef struct qz_gemv_segment {
 int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
                          int blocksize, int blocksize2, const float *lut, void *stream);
 
+/* The same launch with the layer's RMSNorm in front (extension; no reference
+ * counterpart): every segment multiplies x' = norm_weight * rmsnorm(x, eps)
+ * (LlamaRMSNorm, modeling_llama.py:62-67), computed once per workgroup in its
+ * prologue and bit-identical to qz_rmsnorm's output, so the outputs equal
+ * qz_rmsnorm followed by qz_gemv_4bit_grouped.  Takes one token of F16/BF16
+ * activations, K % 2048 == 0, K <= 16384, 16-B-aligned x and norm_weight and
+ * full-step scale layouts; anything else returns QZ_ERR_SHAPE (nothing is
+ * launched: run the two calls). */
+int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
+                                 int quant_type, int blocksize, int blocksize2, const float *lut,
+                                 const void *norm_weight, float eps, void *stream);
+
 /* Fused 4-bit GEMM (prefill, modules.py:62-64): Y[T,M] = X[T,K] . W[M,K]^T
  * (+ bias).  W is decoded tile-by-tile into LDS as exactly the values
  * qz_dequantize_4bit would store (fp16/bf16 of code * absmax) and multiplied

@@ -32,6 +32,7 @@ _ll = ctypes.c_longlong
 _f = ctypes.c_float
 
 GEMV_MAX_SEGMENTS = 4  # QZ_GEMV_MAX_SEGMENTS
+QZ_ERR_SHAPE = -3
 
 
 class GemvSegment(ctypes.Structure):
@@ -56,6 +57,7 @@ SIGNATURES = {
     "cdequantize_blockwise_fp32_stream": [_p, _p, _p, _p, _i, _i, _p],
     "qz_gemv_4bit": [_i, _i, _p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _ll, _p, _p, _p, _p],
     "qz_gemv_4bit_grouped": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p],
+    "qz_gemv_4bit_grouped_rmsnorm": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p, _f, _p],
     "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p, _ll, _p],
     "qz_gemm_4bit_workspace_size": [_i, _i, _i],
     "qz_gemm_16bit": [_i, _i, _i, _p, _i, _i, _p, _p, _p, _i, _p],

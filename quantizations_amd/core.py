@@ -436,13 +436,18 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     return out
 
 
-def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> list:
+def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> list:
     """Several batch-1 4-bit GEMVs that share the input vector A, in ONE launch
     (qz_gemv_4bit_grouped).  items: sequence of
     (B, state, bias[, block_base[, out]]) with equal K, quant_type, blocksize
     and scale format; returns [y_i] as gemv_4bit(A, B_i, state=state_i,
     bias=bias_i, block_base=...) would (`out`, if given, is written in place:
-    a contiguous tensor of M_i elements)."""
+    a contiguous tensor of M_i elements).
+
+    norm=(weight, eps): A is the INPUT of a Llama RMSNorm and every GEMV takes
+    layer_ops.rms_norm(A, weight, eps) -- computed inside the same launch
+    (qz_gemv_4bit_grouped_rmsnorm, bit-identical to the separate norm) where the
+    kernel takes the shape, else as two launches."""
     items = list(items)
     if not 1 <= len(items) <= _lib.GEMV_MAX_SEGMENTS:
         raise ValueError(f"gemv_4bit_grouped takes 1..{_lib.GEMV_MAX_SEGMENTS} weights, got {len(items)}")
@@ -474,8 +479,19 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None) -> l
         segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, block_base, ptr(bias), ptr(y))
         outs.append(y)
     bs2 = int(s0.state2.blocksize) if s0.nested else 0
-    check(lib.qz_gemv_4bit_grouped(len(items), ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
-                                   _gemv_quant_type(s0.quant_type, exact_codes, A.dtype), s0.blocksize, bs2, 0,
+    qt = _gemv_quant_type(s0.quant_type, exact_codes, A.dtype)
+    segp = ctypes.cast(segs, ctypes.c_void_p)
+    if norm is not None:
+        nw, eps = norm
+        if nw.dtype == A.dtype and nw.is_cuda and nw.is_contiguous() and nw.numel() == K:
+            rc = lib.qz_gemv_4bit_grouped_rmsnorm(len(items), segp, K, ptr(A), dtype_code(A.dtype), qt, s0.blocksize,
+                                                  bs2, 0, ptr(nw), float(eps), _lib.stream_of(A))
+            if rc != _lib.QZ_ERR_SHAPE:
+                check(rc, "gemv_4bit_grouped(norm)")
+                return outs
+        from .layer_ops import rms_norm
+        A = rms_norm(A, nw, eps).contiguous()   # shapes the fused launch does not take: two launches
+    check(lib.qz_gemv_4bit_grouped(len(items), segp, K, ptr(A), dtype_code(A.dtype), qt, s0.blocksize, bs2, 0,
                                    _lib.stream_of(A)),
           "gemv_4bit_grouped")
     return outs

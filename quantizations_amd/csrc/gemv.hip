@@ -211,6 +211,8 @@ struct GemvParams {
   int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12), 2 = exact NF4 (CL) precomputed byte table;
                      // lut != nullptr builds an exact (CL) table in kernel
   uint32_t tab[8];
+  const void *nw;    // fused pre-norm (NRM): the RMSNorm weight [K], or nullptr
+  float eps;         //   and its epsilon
 };
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -302,6 +304,8 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   p.tabsel = keep_s(in.tabsel);
 #pragma unroll
   for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
+  p.nw = keep_sp(in.nw);
+  p.eps = keep_s(in.eps);
   return p;
 }
 
@@ -749,9 +753,69 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
   }
 };
 
+// Fused pre-norm (NRM): the bit-exact sum of squares of k_rmsnorm (layer_ops.hip): thread t adds
+// the squares of 16-B chunks t, t + 256, ... in element order, then the xor butterfly of the wave
+template <int DT> __device__ __forceinline__ float norm_chunk_ss(const u32x4 &v, float ss) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t b = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    const float h = DT == QZ_DT_F16 ? __half2float(__ushort_as_half((unsigned short)b)) : __uint_as_float(b << 16);
+    ss = __fadd_rn(ss, __fmul_rn(h, h));
+  }
+  return ss;
+}
+__device__ __forceinline__ float norm_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+// x' = storage(w * storage(x * rs)) for the 8 elements of a 16-B chunk (k_rmsnorm's second pass)
+template <int DT> __device__ __forceinline__ u32x4 norm_chunk_apply(const u32x4 &xv, const u32x4 &wv, float rs) {
+  const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    float r2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t xb = (xw[d] >> (16 * h)) & 0xFFFFu, wb = (ww[d] >> (16 * h)) & 0xFFFFu;
+      // x * rs rounded to fp32, then to the storage dtype (torch's two roundings; the asm keeps
+      // hipcc from folding the multiply into one v_fma_mix rounding), then the weight product
+      float xs = __fmul_rn(DT == QZ_DT_F16 ? __half2float(__ushort_as_half((unsigned short)xb)) : __uint_as_float(xb << 16),
+                           rs);
+      asm volatile("" : "+v"(xs));
+      if constexpr (DT == QZ_DT_F16) {
+        const float hn = __half2float(__float2half_rn(xs));
+        r2[h] = __fmul_rn(__half2float(__ushort_as_half((unsigned short)wb)), hn);
+      } else {
+        const float hn = __bfloat162float(__float2bfloat16(xs));
+        r2[h] = __fmul_rn(__uint_as_float(wb << 16), hn);
+      }
+      asm volatile("" : "+v"(r2[h]));
+    }
+    if constexpr (DT == QZ_DT_F16)
+      o[d] = (uint32_t)__half_as_ushort(__float2half_rn(r2[0])) | ((uint32_t)__half_as_ushort(__float2half_rn(r2[1])) << 16);
+    else
+      o[d] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(r2[0])) |
+             ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(r2[1])) << 16);
+  }
+  return u32x4{o[0], o[1], o[2], o[3]};
+}
+// LDS image of x' (NRM): step s's 2048 activations in a 4 KiB block, lane l's 64-B slice at 64 l,
+// its 16-B chunk i at position i ^ ((l >> 2) & 3) -- the four ds_read_b128 of a step are then
+// conflict-free in every lane group
+__device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = element / 8
+  const uint32_t s = chunk >> 8, l = (chunk >> 2) & 63u, i = chunk & 3u;
+  return (s << 12) + (l << 6) + ((i ^ ((l >> 2) & 3u)) << 4);
+}
+
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false>
+          bool CL = false, bool WT = false, bool NRM = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
+  // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
+  static_assert(!NRM || (NW == 4 && FS && !XL && MODE == kModeTab && (DT == QZ_DT_F16 || DT == QZ_DT_BF16)),
+                "fused pre-norm: 4 waves, full steps, 16-bit activations");
   // WT ("wide table"): 256 B per byte value -- 64 copies of a 4-B entry, or 32 copies of an
   // 8-B exact entry, 64 KiB -- so the lookup address is one v_perm and every copy is bank-private
   constexpr int kPieces = WT ? 16 : kTabCopies / 4;
@@ -825,14 +889,36 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  // 1d. NRM: this thread's chunks of x (L2-resident), ahead of the weights; they are read again
+  // (with the norm weight) after the barrier instead of being held across it
+  constexpr int kNChunks = NRM ? 8 : 1;   // up to 8 x 256 chunks of 8: K <= 16384
+  u32x4 nx[kNChunks];
+  const int n_nchunk = p.K >> 3;
+  if constexpr (NRM) {
+#pragma unroll
+    for (int i = 0; i < kNChunks; ++i) {
+      const int c = (int)threadIdx.x + 256 * i;
+      if (c < n_nchunk) nx[i] = reinterpret_cast<const u32x4 *>(p.x)[c];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // 2. this wave's first step of HBM traffic
-  StepLoads<MODE, DQ, DT, R, XL, ABL, FS> cur;
+  StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> cur;
   int s = wk;
   cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
   const bool have = s < nsteps;
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
     if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
+  }
+  __shared__ float s_nss[NRM ? 4 : 1];
+  if constexpr (NRM) {  // sum of squares: per thread in chunk order, per wave by the xor butterfly
+    float ss = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kNChunks; ++i)
+      if ((int)threadIdx.x + 256 * i < n_nchunk) ss = norm_chunk_ss<DT>(nx[i], ss);
+    ss = norm_wave_sum(ss);
+    if (lane == 0) s_nss[wave] = ss;
   }
   if constexpr (XL) {  // x -> LDS (the launcher guarantees K * XB <= kXLChunks * 16 * NW * 64)
 #pragma unroll
@@ -887,6 +973,20 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
   }
   if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
+  if constexpr (NRM) {  // rs as k_rmsnorm (torch MeanOps: sum * (1/N), then rsqrt(var + eps)); x' -> LDS
+    const float tot = __fadd_rn(__fadd_rn(s_nss[0], s_nss[1]), __fadd_rn(s_nss[2], s_nss[3]));
+    const float rs = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)p.K), p.eps));
+#pragma unroll
+    for (int i = 0; i < kNChunks; ++i) {
+      const int c = (int)threadIdx.x + 256 * i;
+      if (c < n_nchunk) {
+        const u32x4 xv = reinterpret_cast<const u32x4 *>(p.x)[c];
+        const u32x4 wv = reinterpret_cast<const u32x4 *>(p.nw)[c];
+        *reinterpret_cast<u32x4 *>(s_x + norm_x_off((uint32_t)c)) = norm_chunk_apply<DT>(xv, wv, rs);
+      }
+    }
+    __syncthreads();
+  }
   QZ_STAMP(1);
   const uint32_t jb = WT ? (kWide ? (uint32_t)(lane & 31) << 3 : (uint32_t)lane << 2)
                         : (kWide ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2);
@@ -900,8 +1000,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // conditional prefetch makes hipcc's waitcnt pass pick the count valid on
   // both paths -- vmcnt(0) -- which waits for the prefetch itself and
   // serialises HBM traffic with the decode.)
-  auto consume = [&](const StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &c) {
-    if constexpr (XL) const_cast<StepLoads<MODE, DQ, DT, R, XL, ABL, FS> &>(c).xs.load_lds(s_x, c.xb);
+  typedef StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> Loads;
+  auto consume = [&](const Loads &c) {
+    if constexpr (XL) const_cast<Loads &>(c).xs.load_lds(s_x, c.xb);
+    if constexpr (NRM) {
+      auto &raw = const_cast<Loads &>(c).xs.raw;
+      const uint32_t c0 = (uint32_t)c.xb >> 3;  // the lane's first chunk
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(s_x + norm_x_off(c0 + (uint32_t)i));
+        raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+      }
+    }
     uint32_t hi[16], lo[kSplit ? 16 : 1];
     float usc;
     c.xs.prepare(hi, lo, usc);
@@ -927,7 +1037,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // reads the same registers on every path, so no copies are needed.
   if (have) {
     const int n = (nsteps - wk + WK - 1) / WK;  // this wave's steps: s = wk, wk + WK, ...
-    StepLoads<MODE, DQ, DT, R, XL, ABL, FS> other;
+    Loads other;
     int j = 0;
     for (; j + 2 < n; j += 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
@@ -1138,7 +1248,7 @@ struct GemvGroup {
   int nseg;
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL>
+template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -1151,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL>(seg, b - start);
+  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, false, NRM>(seg, b - start);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -1361,6 +1471,8 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   p->K = K;
   p->bs_log2 = bsl;
   p->bs2_log2 = bs2l;
+  p->nw = nullptr;
+  p->eps = 0.0f;
   *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
             (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
             (long long)M * K + 2LL * 1024 < (1LL << 32) &&            // 32-bit element offsets
@@ -1410,8 +1522,10 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   return QZ_OK;
 }
 
-extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
-                                    int quant_type, int blocksize, int blocksize2, const float *lut, void *stream) {
+// nw != nullptr: x is first RMSNorm'd with weight nw / epsilon eps, bit-identically to qz_rmsnorm
+// (the pre-norm of q/k/v and gate/up fused into their grouped launch)
+static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
+                             int blocksize, int blocksize2, const float *lut, const void *nw, float eps, void *stream) {
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
   GemvGroup g;
   g.nseg = nseg;
@@ -1430,6 +1544,16 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
     total_m += q.M;
   }
   if (total_m == 0) return QZ_OK;
+  if (nw) {  // the fused pre-norm takes full-step 16-bit single-token launches only
+    if (!all_vec || total_m > INT32_MAX || (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) || K % 8 != 0 || K > 16384 ||
+        ((uintptr_t)x | (uintptr_t)nw) % 16 != 0)
+      return QZ_ERR_SHAPE;
+    for (int i = 0; i < nseg; ++i) {
+      if (!full_steps(K, blocksize, blocksize2, dq, segs[i].block_base)) return QZ_ERR_SHAPE;
+      g.seg[i].nw = nw;
+      g.seg[i].eps = eps;
+    }
+  }
   if (!all_vec || total_m > INT32_MAX) {  // odd shapes: one launch per segment (same results)
     for (int i = 0; i < nseg; ++i) {
       const qz_gemv_segment &q = segs[i];
@@ -1474,11 +1598,44 @@ extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K
     else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_);    \
     else QZ_GR_RW(DQ_, QZ_DT_F32, FS_);                              \
   } while (0)
-  if (all_fs) { if (dq) QZ_GR_DT(true, true); else QZ_GR_DT(false, true); }
+#define QZ_GN(DQ_, DT_, RR, WW, CL_)                                                                            \
+  hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true>), dim3(blocks), dim3(256), \
+                     (size_t)K * 2, s, g)
+#define QZ_GN_RW(DQ_, DT_, CL_)                                      \
+  do {                                                               \
+    if (R == 4 && WK == 2) QZ_GN(DQ_, DT_, 4, 2, CL_);               \
+    else if (R == 4) QZ_GN(DQ_, DT_, 4, 1, CL_);                     \
+    else if (R == 2) QZ_GN(DQ_, DT_, 2, 1, CL_);                     \
+    else if (WK == 1) QZ_GN(DQ_, DT_, 1, 1, CL_);                    \
+    else if (WK == 2) QZ_GN(DQ_, DT_, 1, 2, CL_);                    \
+    else QZ_GN(DQ_, DT_, 1, 4, CL_);                                 \
+  } while (0)
+  if (nw) {
+    if (dtype == QZ_DT_F16) {
+      if (dq) { if (cl) QZ_GN_RW(true, QZ_DT_F16, true); else QZ_GN_RW(true, QZ_DT_F16, false); }
+      else { if (cl) QZ_GN_RW(false, QZ_DT_F16, true); else QZ_GN_RW(false, QZ_DT_F16, false); }
+    } else {
+      if (dq) QZ_GN_RW(true, QZ_DT_BF16, false); else QZ_GN_RW(false, QZ_DT_BF16, false);
+    }
+  } else if (all_fs) { if (dq) QZ_GR_DT(true, true); else QZ_GR_DT(false, true); }
   else { if (dq) QZ_GR_DT(true, false); else QZ_GR_DT(false, false); }
+#undef QZ_GN_RW
+#undef QZ_GN
 #undef QZ_GR_DT
 #undef QZ_GR_RW
 #undef QZ_GR
   QZ_LAUNCH_CHECK();
   return QZ_OK;
+}
+
+extern "C" int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
+                                    int quant_type, int blocksize, int blocksize2, const float *lut, void *stream) {
+  return gemv_grouped_impl(nseg, segs, K, x, dtype, quant_type, blocksize, blocksize2, lut, nullptr, 0.0f, stream);
+}
+
+extern "C" int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
+                                            int quant_type, int blocksize, int blocksize2, const float *lut,
+                                            const void *norm_weight, float eps, void *stream) {
+  if (!norm_weight || !x) return QZ_ERR_ARG;
+  return gemv_grouped_impl(nseg, segs, K, x, dtype, quant_type, blocksize, blocksize2, lut, norm_weight, eps, stream);
 }

@@ -19,10 +19,15 @@
 namespace qz {
 namespace {
 
+// The fp32 value is pinned in a register first: otherwise hipcc folds a preceding __fmul_rn
+// into the conversion (v_fma_mixlo_f16 a, b, 0), rounding the exact product to 16 bits ONCE,
+// where torch rounds it to fp32 and then to the storage dtype (a different result whenever
+// that double rounding differs, ~1 element in 1000 of an RMSNorm output).
 template <int DT> __device__ __forceinline__ float round_dt(float v) {
+  if constexpr (DT == QZ_DT_F32) return v;
+  asm volatile("" : "+v"(v));
   if constexpr (DT == QZ_DT_F16) return __half2float(__float2half_rn(v));
-  else if constexpr (DT == QZ_DT_BF16) return __bfloat162float(__float2bfloat16(v));
-  else return v;
+  else return __bfloat162float(__float2bfloat16(v));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -76,7 +81,9 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, con
       const float v = value(e);
       if constexpr (ADD) store_f32<DT>(sr, e, v);                     // the new residual stream
       const float h = round_dt<DT>(__fmul_rn(v, rs));                  // hidden.to(input_dtype)
-      store_f32<DT>(yr, e, __fmul_rn(load_f32<DT>(w, e), h));          // weight * hidden
+      float o = __fmul_rn(load_f32<DT>(w, e), h);                      // weight * hidden (exact for
+      asm volatile("" : "+v"(o));                                      // 16-bit dtypes; pinned anyway)
+      store_f32<DT>(yr, e, o);
     }
   }
 }

@@ -118,9 +118,65 @@ def fuse_projection_groups(model: nn.Module, groups=DEFAULT_PROJECTION_GROUPS) -
 
 
 def unfuse_projection_groups(model: nn.Module) -> None:
-    """Remove every DecodeGroup attached by fuse_projection_groups."""
+    """Remove every DecodeGroup attached by fuse_projection_groups (and with them any RMSNorm
+    fuse_prenorm absorbed into one)."""
+    unfuse_prenorm(model)
     for m in model.modules():
         m.__dict__.pop("_qz_group", None)
+
+
+def _identity(x):
+    return x
+
+
+def fuse_prenorm(model: nn.Module) -> int:
+    """Absorb each decoder layer's input_layernorm into its q/k/v decode group and its
+    post_attention_layernorm into its gate/up group (DecodeGroup.prenorm).  The norm module
+    then returns its input unchanged, and the group's single-token launch normalises x in its
+    prologue (qz_gemv_4bit_grouped_rmsnorm, bit-identical to the separate qz_rmsnorm launch):
+    one launch fewer per norm.  Other inputs (prefill, small batches) run the norm as the model
+    did before, then the group.  In a LlamaDecoderLayer these norms feed nothing else
+    (modeling_llama.py:306-321).  Call after fuse_projection_groups (and fuse_layer_ops);
+    layers whose norm, groups or decoder forward do not match are left alone.  Returns the
+    number of norms absorbed."""
+    n = 0
+    for layer in model.modules():
+        if type(layer).__name__ not in DECODER_CLASSES or "_qz_fused_decoder" in layer.__dict__:
+            continue
+        attn, mlp = getattr(layer, "self_attn", None), getattr(layer, "mlp", None)
+        pairs = (("input_layernorm", attn, ("q_proj", "k_proj", "v_proj")),
+                 ("post_attention_layernorm", mlp, ("gate_proj", "up_proj")))
+        for ln_name, parent, names in pairs:
+            ln = getattr(layer, ln_name, None)
+            if ln is None or parent is None or type(ln).__name__ not in RMSNORM_CLASSES or \
+                    "_qz_absorbed_norm" in ln.__dict__ or not hasattr(ln, "variance_epsilon"):
+                continue
+            w = getattr(ln, "weight", None)
+            members = [getattr(parent, nm, None) for nm in names]
+            g = members[0].__dict__.get("_qz_group") if isinstance(members[0], Linear4bit) else None
+            if w is None or not w.is_cuda or g is None or g.prenorm is not None or \
+                    g._compute is not _linear4bit_group_compute or \
+                    [id(m) for m in g.members] != [id(m) for m in members]:
+                continue
+            g.prenorm = (w, float(ln.variance_epsilon), ln.forward)   # the norm as the model runs it now
+            ln.__dict__["_qz_absorbed_norm"] = ln.__dict__.get("forward")
+            ln.__dict__["forward"] = _identity
+            n += 1
+    return n
+
+
+def unfuse_prenorm(model: nn.Module) -> None:
+    """Undo fuse_prenorm: every absorbed norm computes again, no group applies one."""
+    for m in model.modules():
+        if "_qz_absorbed_norm" in m.__dict__:
+            prev = m.__dict__.pop("_qz_absorbed_norm")
+            if prev is None:
+                m.__dict__.pop("forward", None)
+            else:
+                m.__dict__["forward"] = prev
+        g = m.__dict__.get("_qz_group")
+        if g is not None:
+            g.prenorm = None
 
 
 # ---------------------------------------------------------------------------
@@ -253,9 +309,11 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
 
 
 def unfuse_layer_ops(model: nn.Module) -> None:
-    """Undo fuse_layer_ops (norm forwards and every patched apply_rotary_pos_emb)."""
+    """Undo fuse_layer_ops (norm forwards and every patched apply_rotary_pos_emb) and any
+    fuse_prenorm on top of it."""
     import sys
 
+    unfuse_prenorm(model)
     for m in model.modules():
         if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None) or \
                 m.__dict__.pop("_qz_fused_decoder", None):

@@ -46,6 +46,9 @@ class DecodeGroup:
         self._x = None                   # weakref to the input the cached outputs belong to
         self._ver = -1
         self._outs = {}
+        # (weight, eps, fn): the members' input is the input of this RMSNorm, absorbed into the
+        # group by integration.fuse_prenorm (fn(x) = the norm as the model computed it)
+        self.prenorm = None
 
     @staticmethod
     def accepts(x: torch.Tensor) -> bool:
@@ -75,13 +78,19 @@ class DecodeGroup:
 def _linear4bit_group_compute(group: DecodeGroup, x: torch.Tensor):
     m0 = group.members[0]
     inp_dtype = x.dtype
+    norm = group.prenorm
+    fused_norm = (norm is not None and x.numel() == x.shape[-1] and m0._input(x) is x and x.is_cuda
+                  and norm[0].dtype == x.dtype and norm[0].is_contiguous() and norm[0].numel() == x.shape[-1])
+    if norm is not None and not fused_norm:
+        x = norm[2](x)                   # the absorbed RMSNorm as its own launch
     xin = m0._input(x)
     items = []
     for m in group.members:
         bias = None if m.bias is None else m.bias.to(xin.dtype)
         items.append((m.weight, m.weight.quant_state, bias))
     if xin.numel() == xin.shape[-1]:
-        outs = gemv_4bit_grouped(xin, items, exact_codes=exact_codes_for(m0.compute_dtype))
+        outs = gemv_4bit_grouped(xin, items, exact_codes=exact_codes_for(m0.compute_dtype),
+                                 norm=norm[:2] if fused_norm else None)
     elif grouped_tokens_ok(xin, items):
         outs = gemm_4bit_grouped(xin, items)
     else:  # shapes the multi-token kernel does not take: each member as it would run alone
@@ -130,6 +139,8 @@ class Linear4bit(nn.Linear):
         group = self.__dict__.get("_qz_group")
         if group is not None and group.accepts(x):
             return group.take(self, x)
+        if group is not None and group.prenorm is not None:
+            x = group.prenorm[2](x)      # prefill through a group that absorbed its RMSNorm
         inp_dtype = x.dtype
         xin = self._input(x)
         bias = None if self.bias is None else self.bias.to(xin.dtype)

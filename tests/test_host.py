@@ -124,6 +124,40 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     assert not rope_supported(q, q, torch.randn(1, 3, 16), torch.randn(1, 3, 16))
 
 
+def test_fuse_prenorm_absorbs_only_cuda_norms_of_plain_groups():
+    """fuse_prenorm needs a Linear4bit decode group (not a row-sharded one) and a norm weight
+    on the GPU: on a CPU model it absorbs nothing; a group whose compute is not the Linear4bit
+    one is never given a norm; unfuse_prenorm leaves no patched forward behind."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.integration import fuse_prenorm, unfuse_prenorm
+    from quantizations_amd.modules import DecodeGroup, _linear4bit_group_compute
+
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=97)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).eval()
+    for layer in model.model.layers:   # Linear4bit projections (unquantised on CPU) in decode groups
+        for parent, names in ((layer.self_attn, ("q_proj", "k_proj", "v_proj")), (layer.mlp, ("gate_proj", "up_proj"))):
+            members = []
+            for nm in names:
+                lin = getattr(parent, nm)
+                q = qa.Linear4bit(lin.in_features, lin.out_features, bias=False, quant_type="nf4")
+                setattr(parent, nm, q)
+                members.append(q)
+            grp = DecodeGroup(members, _linear4bit_group_compute)
+            for q in members:
+                q.__dict__["_qz_group"] = grp
+    assert fuse_prenorm(model) == 0                      # norm weights on the CPU
+    assert not any("_qz_absorbed_norm" in m.__dict__ for m in model.modules())
+    g = model.model.layers[0].self_attn.q_proj.__dict__["_qz_group"]
+    assert isinstance(g, DecodeGroup) and g.prenorm is None
+    g._compute = lambda grp, x: None                     # e.g. a row-sharded group's compute
+    assert fuse_prenorm(model) == 0 and g.prenorm is None
+    unfuse_prenorm(model)
+    assert not any("forward" in m.__dict__ for m in model.modules())
+
+
 def test_fuse_layer_ops_leaves_other_rotary_forms_alone():
     """The rotary patch is limited to Llama/Mistral/Qwen2 attention modules whose
     modeling module has the half-split rotate_half.  An attention class outside

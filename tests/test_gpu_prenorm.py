@@ -97,11 +97,18 @@ def _llama(seed=5):
 
 
 def test_llama_prenorm_logits_and_tokens_bit_identical_eager_and_graph():
-    from transformers.cache_utils import StaticCache
-
-    from quantizations_amd.integration import fuse_prenorm, unfuse_prenorm
+    from quantizations_amd.integration import fuse_prenorm, unfuse_layer_ops, unfuse_prenorm
 
     model, cfg = _llama()
+    try:
+        _check_prenorm_model(model, cfg, fuse_prenorm, unfuse_prenorm)
+    finally:
+        unfuse_layer_ops(model)   # the modeling module's apply_rotary_pos_emb is process-global
+
+
+def _check_prenorm_model(model, cfg, fuse_prenorm, unfuse_prenorm):
+    from transformers.cache_utils import StaticCache
+
     ids = torch.randint(0, cfg.vocab_size, (1, 10), device=DEV, generator=torch.Generator(device="cuda").manual_seed(3))
 
     def greedy(n):

@@ -889,16 +889,23 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // 1d. NRM: this thread's chunks of x (L2-resident), ahead of the weights; they are read again
-  // (with the norm weight) after the barrier instead of being held across it
+  // 1d. NRM: this thread's chunks of x and of the norm weight (L2-resident), ahead of the
+  // weights.  The first kNHeld chunks (K <= 4096: all of them) stay in registers across the
+  // barrier; later ones are read again after it (registers would cost occupancy)
   constexpr int kNChunks = NRM ? 8 : 1;   // up to 8 x 256 chunks of 8: K <= 16384
-  u32x4 nx[kNChunks];
+  constexpr int kNHeld = NRM ? 2 : 1;
+  u32x4 nx[kNChunks], nwh[kNHeld];
   const int n_nchunk = p.K >> 3;
   if constexpr (NRM) {
 #pragma unroll
     for (int i = 0; i < kNChunks; ++i) {
       const int c = (int)threadIdx.x + 256 * i;
       if (c < n_nchunk) nx[i] = reinterpret_cast<const u32x4 *>(p.x)[c];
+    }
+#pragma unroll
+    for (int i = 0; i < kNHeld; ++i) {
+      const int c = (int)threadIdx.x + 256 * i;
+      if (c < n_nchunk) nwh[i] = reinterpret_cast<const u32x4 *>(p.nw)[c];
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -980,8 +987,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     for (int i = 0; i < kNChunks; ++i) {
       const int c = (int)threadIdx.x + 256 * i;
       if (c < n_nchunk) {
-        const u32x4 xv = reinterpret_cast<const u32x4 *>(p.x)[c];
-        const u32x4 wv = reinterpret_cast<const u32x4 *>(p.nw)[c];
+        const u32x4 xv = i < kNHeld ? nx[i] : reinterpret_cast<const u32x4 *>(p.x)[c];
+        const u32x4 wv = i < kNHeld ? nwh[i < kNHeld ? i : 0] : reinterpret_cast<const u32x4 *>(p.nw)[c];
         *reinterpret_cast<u32x4 *>(s_x + norm_x_off((uint32_t)c)) = norm_chunk_apply<DT>(xv, wv, rs);
       }
     }

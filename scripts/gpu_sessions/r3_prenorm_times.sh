@@ -1,0 +1,7 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u scripts/dev/prenorm_times.py > gpurun_out/r3p_times.txt 2>&1 || { tail -20 gpurun_out/r3p_times.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/r3p_times.txt

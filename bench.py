@@ -450,9 +450,10 @@ assert gemv_alg_bytes([(4096, 4096)]) == GEMV_BYTES_4096
 
 
 @torch.inference_mode()
-def dominant_roofline(copies: int = 8, iters: int = 100):
+def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True):
     """The decode step's longest Linear4bit launch: the grouped gate/up GEMV of a
-    Llama-3-8B layer (2 x 14336x4096 NF4+DQ in ONE launch), rotating weights
+    Llama-3-8B layer (2 x 14336x4096 NF4+DQ in ONE launch; with `prenorm`, the
+    post-attention RMSNorm inside it, as the bench decode runs it), rotating weights
     (8 sets = 485 MB > the 256 MiB Infinity Cache), same timing method."""
     from quantizations_amd.core import gemv_4bit_grouped, quantize_4bit
 
@@ -468,34 +469,40 @@ def dominant_roofline(copies: int = 8, iters: int = 100):
         sets.append(items)
         del W
     x = torch.randn(1, 1, 4096, device=dev).to(torch.float16)
+    nw = (1.0 + 0.1 * torch.randn(4096, device=dev)).to(torch.float16)
     outs = [torch.empty(14336, device=dev, dtype=torch.float16) for _ in range(2)]
     sets = [[(p, q, b, 0, o) for (p, q, b), o in zip(items, outs)] for items in sets]
     from quantizations_amd.core import exact_codes_for
 
-    def timed(exact):
+    def timed(exact, norm):
+        nm = (nw, 1e-5) if norm else None
         for i in range(2 * copies):
-            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact)
+            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact, norm=nm)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(100_000_000)
         e0.record()
         for i in range(iters):
-            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact)
+            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact, norm=nm)
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / iters
 
     prod = exact_codes_for(torch.float32)      # the bench model's Linear4bit (compute_dtype fp32)
-    us = timed(prod)
-    other_us = timed(not prod)
-    nbytes = gemv_alg_bytes([(14336, 4096)] * 2)
-    return {"kernel": "k_gemv_4bit_grouped gate/up 2 x 14336x4096 NF4+DQ (one launch per layer)",
+    us = timed(prod, prenorm)
+    other_us = timed(not prod, prenorm)
+    plain_us = timed(prod, False) if prenorm else us
+    nbytes = gemv_alg_bytes([(14336, 4096)] * 2) + (4096 * 2 if prenorm else 0)   # + the norm weight
+    return {"kernel": "k_gemv_4bit_grouped gate/up 2 x 14336x4096 NF4+DQ (one launch per layer)"
+                      + (", post-attention RMSNorm in its prologue" if prenorm else ""),
             "codes": "exact (fp32 as hi+lo fp16)" if prod else "fp16",
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-            "other_codes_launch_us": round(other_us, 3), "traffic": _pmc_traffic("r3_gateup_pmc.json"),
-            "profile": "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes)"}
+            "other_codes_launch_us": round(other_us, 3), "without_norm_launch_us": round(plain_us, 3),
+            "traffic": _pmc_traffic("r3_gateup_pmc.json"),
+            "profile": "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the "
+                       "launch without the norm)"}
 
 
 def _pmc_traffic(name: str):
@@ -1031,7 +1038,9 @@ def main():
                 "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
                                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
-                "dominant_decode_kernel": dominant_roofline()}
+                "dominant_decode_kernel": dominant_roofline(
+                    prenorm=bool(not args.no_prenorm and not sharded and not args.no_fuse
+                                 and layer_ops in ("all", "norm")))}
         from quantizations_amd import _lib, core
         ink = gemv_in_kernel(bool(core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32), torch.float16)
                                   & _lib.EXACT_CODES))

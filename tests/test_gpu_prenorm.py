@@ -18,14 +18,14 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-def _items(Ms, K, dtype, seed, bias_seg=None):
+def _items(Ms, K, dtype, seed, bias_seg=None, quant="nf4", dq=True):
     from quantizations_amd.core import quantize_4bit
 
     g = torch.Generator(device="cuda").manual_seed(seed)
     items = []
     for i, M in enumerate(Ms):
         W = (torch.randn(M, K, device=DEV, generator=g) * 0.02).to(dtype)
-        packed, st = quantize_4bit(W, quant_type="nf4", compress_statistics=True)
+        packed, st = quantize_4bit(W, quant_type=quant, compress_statistics=dq)
         b = (torch.randn(M, device=DEV, generator=g) * 0.1).to(dtype) if i == bias_seg else None
         items.append((packed, st, b))
     return items
@@ -49,6 +49,21 @@ def test_grouped_gemv_rmsnorm_bit_identical_to_two_launches(dtype, exact, Ms, K)
     for i, (a, b) in enumerate(zip(got, ref)):
         assert a.shape == b.shape and a.dtype == b.dtype
         assert torch.equal(a, b), f"segment {i}: {(a.float() - b.float()).abs().max().item()}"
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_grouped_gemv_rmsnorm_fp4_without_double_quant(dtype):
+    """Config #3's format (FP4, fp32 absmax): the other scale path of the fused launch."""
+    from quantizations_amd.core import gemv_4bit_grouped
+    from quantizations_amd.layer_ops import rms_norm
+
+    items = _items((4096, 1024, 1024), 4096, dtype, seed=3, quant="fp4", dq=False)
+    x = (torch.randn(1, 1, 4096, device=DEV) * 2).to(dtype)
+    w = (1.0 + 0.1 * torch.randn(4096, device=DEV)).to(dtype)
+    ref = gemv_4bit_grouped(rms_norm(x, w, 1e-6), items)
+    got = gemv_4bit_grouped(x, items, norm=(w, 1e-6))
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
 
 
 def test_grouped_rmsnorm_entry_rejects_what_it_cannot_fuse():

@@ -148,8 +148,9 @@ int qz_gemv_4bit_grouped(int nseg, const qz_gemv_segment *segs, int K, const voi
  * prologue and bit-identical to qz_rmsnorm's output, so the outputs equal
  * qz_rmsnorm followed by qz_gemv_4bit_grouped.  Takes one token of F16/BF16
  * activations, K % 2048 == 0, K <= 16384, 16-B-aligned x and norm_weight and
- * full-step scale layouts; anything else returns QZ_ERR_SHAPE (nothing is
- * launched: run the two calls). */
+ * full-step scale layouts, and launches of at most 4096 workgroups (each one
+ * repeats the norm; beyond that the two calls are faster); anything else
+ * returns QZ_ERR_SHAPE (nothing is launched: run the two calls). */
 int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype,
                                  int quant_type, int blocksize, int blocksize2, const float *lut,
                                  const void *norm_weight, float eps, void *stream);

@@ -1531,6 +1531,7 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
 
 // nw != nullptr: x is first RMSNorm'd with weight nw / epsilon eps, bit-identically to qz_rmsnorm
 // (the pre-norm of q/k/v and gate/up fused into their grouped launch)
+constexpr int kNormMaxBlocks = 4096;
 static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
                              int blocksize, int blocksize2, const float *lut, const void *nw, float eps, void *stream) {
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
@@ -1580,6 +1581,11 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }
   for (int i = nseg; i < kMaxSeg; ++i) g.start[i] = blocks;
+  // every workgroup repeats the norm prologue (x and the norm weight from L2, two barriers, 8 KiB
+  // more LDS): past ~4096 workgroups it costs more than the separate launch saves (measured:
+  // Llama-3-70B gate/up, 7168 workgroups, 74.6 us fused vs 58.6 us for the two launches;
+  // profiles/r3_prenorm_launch_times.txt)
+  if (nw && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
   bool all_fs = true;
   for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;

@@ -37,10 +37,11 @@ def graph_time(fn, reps=64, iters=20):
     return ts[len(ts) // 2]
 
 
-for name, Ms in (("qkv", (4096, 1024, 1024)), ("gateup", (14336, 14336))):
-    items = _items(Ms, 4096, torch.float16, seed=1)
-    x = torch.randn(1, 1, 4096, device=DEV).half()
-    w = (1 + 0.1 * torch.randn(4096, device=DEV)).half()
+for name, Ms, K in (("qkv", (4096, 1024, 1024), 4096), ("gateup", (14336, 14336), 4096),
+                    ("qkv70b", (8192, 1024, 1024), 8192), ("gateup70b", (28672, 28672), 8192)):
+    items = _items(Ms, K, torch.float16, seed=1)
+    x = torch.randn(1, 1, K, device=DEV).half()
+    w = (1 + 0.1 * torch.randn(K, device=DEV)).half()
     outs = [torch.empty(M, device=DEV, dtype=torch.float16) for M in Ms]
     it = [(a, b, c, 0, o) for (a, b, c), o in zip(items, outs)]
     t_g = graph_time(lambda: gemv_4bit_grouped(x, it, exact_codes=True))

@@ -33,7 +33,8 @@ def _items(Ms, K, dtype, seed, bias_seg=None, quant="nf4", dq=True):
 
 @pytest.mark.parametrize("dtype,exact", [(torch.float16, None), (torch.float16, True), (torch.bfloat16, None)])
 @pytest.mark.parametrize("Ms,K", [((4096, 1024, 1024), 4096), ((14336, 14336), 4096), ((2048, 512, 512), 2048),
-                                  ((8192, 1024, 1024), 8192), ((3000, 8), 4096)])
+                                  ((8192, 1024, 1024), 8192), ((3000, 8), 4096),
+                                  ((28672, 28672), 8192)])   # 7168 workgroups: two launches instead
 def test_grouped_gemv_rmsnorm_bit_identical_to_two_launches(dtype, exact, Ms, K):
     from quantizations_amd.core import gemv_4bit_grouped
     from quantizations_amd.layer_ops import rms_norm

@@ -294,6 +294,26 @@ int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long
  * contiguous elements of `dtype` (torch's two rounded elementwise ops). */
 int qz_silu_mul(const void *gate, const void *up, int dtype, long long n, void *y, void *stream);
 
+/* One new token of LlamaAttention.forward (modeling_llama.py:243-281) against a static KV
+ * cache, from the q/k/v projection outputs to the o_proj input, in one launch (two when
+ * L > 128): rotary of q and k (qz_rope_qk's arithmetic; the cache receives the same bits),
+ * StaticLayer.update (cache_utils.py:455-487: k_cache/v_cache[b, :, p] = k, v with
+ * p = *pos, then *pos = p + 1) and sdpa_attention_forward's masked GQA attention
+ *   out[b, hq] = softmax_j(mask[b, j] ? (q[b, hq] . k_cache[b, hq / (Hq / Hkv), j]) * scale : -inf) v
+ * in fp32 (scores, probabilities, accumulation), rounded once to `dtype`.
+ *   q [B, Hq*D], k/v [B, Hkv*D]: row strides q_row/k_row/v_row elements, head-major;
+ *   cos/sin [B or 1, D]: row stride cs_row (0: one row for every b);
+ *   k_cache/v_cache [B, Hkv, L, D] contiguous, 16-B aligned; mask bool, (b, j) at
+ *   b*mask_b + j*mask_j; pos int64 (device); arrive: a device uint32 that is 0 before the
+ *   call and is left 0; out [B, Hq*D] with row stride out_row;
+ *   work: L > 128 only, B*Hkv*ceil(L/128)*(Hq/Hkv)*(D+2) floats.
+ * F16/BF16, D in {64, 128}, Hq/Hkv <= 8; otherwise QZ_ERR_SHAPE / QZ_ERR_DTYPE, nothing launched. */
+int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const void *q, long long q_row,
+                        const void *k, long long k_row, const void *v, long long v_row, const void *cos,
+                        const void *sin, long long cs_row, void *k_cache, void *v_cache, const void *mask,
+                        long long mask_b, long long mask_j, long long *pos, unsigned int *arrive, void *out,
+                        long long out_row, float *work, float scale, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

@@ -58,6 +58,8 @@ SIGNATURES = {
     "qz_gemv_4bit": [_i, _i, _p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _ll, _p, _p, _p, _p],
     "qz_gemv_4bit_grouped": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p],
     "qz_gemv_4bit_grouped_rmsnorm": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p, _f, _p],
+    "qz_decode_attention": [_i, _i, _i, _i, _i, _i, _p, _ll, _p, _ll, _p, _ll, _p, _p, _ll, _p, _p, _p, _ll, _ll,
+                            _p, _p, _p, _ll, _p, _f, _p],
     "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p, _ll, _p],
     "qz_gemm_4bit_workspace_size": [_i, _i, _i],
     "qz_gemm_16bit": [_i, _i, _i, _p, _i, _i, _p, _p, _p, _i, _p],

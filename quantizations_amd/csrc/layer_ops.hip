@@ -137,6 +137,243 @@ __global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, co
   store_f32<DT>(y, i, __fmul_rn(a, load_f32<DT>(u, i)));
 }
 
+// ---------------------------------------------------------------------------
+// Decode attention with a static KV cache (LlamaAttention.forward, modeling_llama.py:243-281,
+// for one new token per sequence): rotary of q and k, the cache update of StaticLayer.update
+// (cache_utils.py:455-487: keys/values[:, :, p] = k, v and p += 1) and the masked GQA
+// softmax(q k^T * scale) v of sdpa_attention_forward -- in eager torch 14 launches per layer
+// (rope, arange, two int64 adds, two index_copy_, two repeat_kv copies, the bool-mask
+// conversion, attn_fwd).  Grid (nsplit, Hkv, B): a workgroup takes the G = Hq / Hkv query
+// heads of one kv head over kAttnChunk key positions; nsplit > 1 leaves per-chunk partials
+// (max, sum, unnormalised output) that k_decode_attn_combine merges.
+// Numerics: q and k are rotated with k_rope_qk's per-op rounding (the cache receives the
+// bit-identical k), scores and probabilities stay fp32 (SDPA's flash kernel rounds the
+// probabilities to the storage dtype before P V; this kernel does not), output rounded once.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAttnChunk = 128;  // key positions per workgroup
+constexpr int kAttnMaxG = 8;     // query heads per kv head
+
+struct DecodeAttnArgs {
+  const void *q, *k, *v;     // projection outputs, row b at b * {qs, ks, vs} elements, head-major
+  long long qs, ks, vs;
+  const void *cos, *sin;     // [B or 1, D], row b at b * cs (cs = 0: one row for all)
+  long long cs;
+  void *kc, *vc;             // caches [B, Hkv, L, D], contiguous
+  const unsigned char *mask;  // bool, element (b, j) at b * mb + j * mj
+  long long mb, mj;
+  long long *pos;            // write position p (StaticLayer.cumulative_length), advanced by one
+  unsigned int *arrive;      // arrival counter, zero between launches
+  void *out;                 // [B, Hq * D], row b at b * os
+  long long os;
+  float *part;               // nsplit > 1: [B, Hkv, nsplit, G, D + 2]
+  int Hkv, G, L, nsplit;
+  float scale;
+};
+
+// storage bits of a value (the RNE conversions store_f32 uses) and back
+template <int DT> __device__ __forceinline__ uint32_t bits_dt(float v) {
+  if constexpr (DT == QZ_DT_F16) return f32_to_f16_bits(v);
+  else return __bfloat16_as_ushort(__float2bfloat16(v));
+}
+template <int DT> __device__ __forceinline__ float from_bits(uint32_t u) {
+  if constexpr (DT == QZ_DT_F16) return __half2float(__ushort_as_half((unsigned short)(u & 0xFFFFu)));
+  else return __uint_as_float(u << 16);
+}
+
+template <int DT, int D>
+__global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
+  constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
+  static_assert(ES == 2, "16-bit activations and caches");
+  constexpr int H2 = D / 2;  // rotary half; also the share of a row one thread dots
+  __shared__ float s_q[kAttnMaxG][D];                  // rotated q (storage-rounded values)
+  __shared__ float s_sc[2][kAttnMaxG][kAttnChunk];     // half-row partial scores; [0]: probabilities
+  __shared__ uint32_t s_v[kAttnChunk][H2];             // raw v rows (zero where masked)
+  __shared__ uint32_t s_kn[H2], s_vn[H2];              // the new (rotated) k and v, raw
+  __shared__ unsigned char s_ok[kAttnChunk];
+  __shared__ float s_m[kAttnMaxG], s_l[kAttnMaxG];
+
+  const int t = threadIdx.x, split = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int G = a.G, L = a.L;
+  const int j0 = split * kAttnChunk;
+  const long long p = *a.pos;
+  const bool mine = p >= j0 && p < j0 + kAttnChunk && p < L;  // this chunk holds the new token
+  const long long crow = ((long long)b * a.Hkv + h) * L;     // first cache row of (b, h)
+
+  // 1. rotary of the G query heads (and, in the chunk holding p, of the new key), k_rope_qk's
+  //    arithmetic: q*cos + cat(-x2, x1)*sin with every torch op rounded to the storage dtype
+  const char *cb = reinterpret_cast<const char *>(a.cos) + (long long)b * a.cs * ES;
+  const char *sb = reinterpret_cast<const char *>(a.sin) + (long long)b * a.cs * ES;
+  auto rope = [&](const char *x, int d, float &lo, float &hi) {
+    const float x1 = load_f32<DT>(x, d), x2 = load_f32<DT>(x, d + H2);
+    const float c1 = load_f32<DT>(cb, d), c2 = load_f32<DT>(cb, d + H2);
+    const float s1 = load_f32<DT>(sb, d), s2 = load_f32<DT>(sb, d + H2);
+    lo = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(x1, c1)), round_dt<DT>(__fmul_rn(-x2, s1)))));
+    hi = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(x2, c2)), round_dt<DT>(__fmul_rn(x1, s2)))));
+  };
+  const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)h * G * D) * ES;
+  for (int i = t; i < G * H2; i += 256) {
+    const int g = i / H2, d = i - g * H2;
+    float lo, hi;
+    rope(qb + (long long)g * D * ES, d, lo, hi);
+    s_q[g][d] = lo;
+    s_q[g][d + H2] = hi;
+  }
+  if (mine && t < H2) {
+    const char *kb = reinterpret_cast<const char *>(a.k) + ((long long)b * a.ks + (long long)h * D) * ES;
+    const char *vb = reinterpret_cast<const char *>(a.v) + ((long long)b * a.vs + (long long)h * D) * ES;
+    float lo, hi;
+    rope(kb, t, lo, hi);
+    char *kd = reinterpret_cast<char *>(a.kc) + (crow + p) * D * ES;
+    char *vd = reinterpret_cast<char *>(a.vc) + (crow + p) * D * ES;
+    store_f32<DT>(kd, t, lo);
+    store_f32<DT>(kd, t + H2, hi);
+    const uint32_t vw = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
+    reinterpret_cast<uint32_t *>(vd)[t] = vw;
+    s_vn[t] = vw;
+    // the rotated k as raw elements: element e in the 16-bit half e % 2 of s_kn[e / 2]
+    reinterpret_cast<uint16_t *>(s_kn)[t] = (uint16_t)bits_dt<DT>(lo);
+    reinterpret_cast<uint16_t *>(s_kn)[t + H2] = (uint16_t)bits_dt<DT>(hi);
+  }
+  if (t < kAttnChunk) {
+    const int j = j0 + t;
+    s_ok[t] = (j < L && a.mask[(long long)b * a.mb + (long long)j * a.mj] != 0) ? 1 : 0;
+  }
+  __syncthreads();
+
+  // 2. half-row dot products: thread t scores position t % 128 over dims [H2 * (t / 128), + H2)
+  //    and stages that half of the position's v row in LDS
+  {
+    const int pos = t & (kAttnChunk - 1), half = t >> 7;
+    const long long j = j0 + pos;
+    const bool ok = s_ok[pos] != 0;
+    constexpr int NW = H2 / 2;  // 32-bit words of half a row
+    uint32_t kw[NW], vw[NW];
+    if (ok && j == p) {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) { kw[i] = s_kn[half * NW + i]; vw[i] = s_vn[half * NW + i]; }
+    } else if (ok) {
+      const u32x4 *kr = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.kc) + ((crow + j) * D + half * H2) * ES);
+      const u32x4 *vr = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.vc) + ((crow + j) * D + half * H2) * ES);
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) {
+        const u32x4 x = kr[i], y = vr[i];
+        kw[4 * i] = x.x; kw[4 * i + 1] = x.y; kw[4 * i + 2] = x.z; kw[4 * i + 3] = x.w;
+        vw[4 * i] = y.x; vw[4 * i + 1] = y.y; vw[4 * i + 2] = y.z; vw[4 * i + 3] = y.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) kw[i] = vw[i] = 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) s_v[pos][half * NW + i] = vw[i];
+    for (int g = 0; g < G; ++g) {
+      const float *qg = &s_q[g][half * H2];
+      float acc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        acc = fmaf(from_bits<DT>(kw[i]), qg[2 * i], acc);
+        acc = fmaf(from_bits<DT>(kw[i] >> 16), qg[2 * i + 1], acc);
+      }
+      s_sc[half][g][pos] = acc;
+    }
+  }
+  __syncthreads();
+
+  // 3. softmax statistics: 32 threads per query head, 4 positions each
+  {
+    const int g = t >> 5, i = t & 31;
+    const int gg = g < G ? g : 0;
+    float s[4], m = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pos = 4 * i + r;
+      s[r] = s_ok[pos] ? __fmul_rn(__fadd_rn(s_sc[0][gg][pos], s_sc[1][gg][pos]), a.scale) : -INFINITY;
+      m = fmaxf(m, s[r]);
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+    float l = 0.0f, e[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      e[r] = s[r] == -INFINITY ? 0.0f : expf(s[r] - m);
+      l += e[r];
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, kWave);
+    __syncthreads();  // every read of s_sc[0] above is done before it is overwritten
+    if (g < G) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s_sc[0][g][4 * i + r] = e[r];
+      if (i == 0) { s_m[g] = m; s_l[g] = l; }
+    }
+  }
+  __syncthreads();
+
+  // 4. P V: one output pair (2 dims of one query head) per thread and iteration
+  const int n = min(kAttnChunk, L - j0);
+  for (int o = t; o < G * H2; o += 256) {
+    const int g = o / H2, w = o - g * H2;
+    float acc0 = 0.0f, acc1 = 0.0f;
+    for (int pos = 0; pos < n; ++pos) {
+      const float pr = s_sc[0][g][pos];
+      const uint32_t vv = s_v[pos][w];
+      acc0 = fmaf(pr, from_bits<DT>(vv), acc0);
+      acc1 = fmaf(pr, from_bits<DT>(vv >> 16), acc1);
+    }
+    if (a.nsplit == 1) {
+      const float inv_l = s_l[g];
+      char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)(h * G + g) * D) * ES;
+      store_f32<DT>(ob, 2 * w, __fdiv_rn(acc0, inv_l));
+      store_f32<DT>(ob, 2 * w + 1, __fdiv_rn(acc1, inv_l));
+    } else {
+      float *pp = a.part + ((((long long)b * a.Hkv + h) * a.nsplit + split) * G + g) * (D + 2);
+      pp[2 * w] = acc0;
+      pp[2 * w + 1] = acc1;
+      if (w == 0) { pp[D] = s_m[g]; pp[D + 1] = s_l[g]; }
+    }
+  }
+
+  // 5. the last workgroup to arrive advances the cache position (every workgroup has read p)
+  __syncthreads();
+  if (t == 0) {
+    const unsigned int total = gridDim.x * gridDim.y * gridDim.z;
+    if (atomicAdd(a.arrive, 1u) == total - 1u) {
+      *a.pos = p + 1;
+      atomicExch(a.arrive, 0u);
+    }
+  }
+}
+
+// nsplit > 1: merge the chunk partials of one (b, kv head) -- out = sum_s e^(m_s - M) o_s /
+// sum_s e^(m_s - M) l_s with M = max_s m_s; empty chunks (m_s = -inf) weigh nothing
+template <int DT, int D>
+__global__ __launch_bounds__(256) void k_decode_attn_combine(DecodeAttnArgs a) {
+  constexpr int ES = 2;
+  const int h = blockIdx.x, b = blockIdx.y, G = a.G;
+  const float *base = a.part + ((long long)b * a.Hkv + h) * a.nsplit * G * (D + 2);
+  for (int o = threadIdx.x; o < G * D; o += 256) {
+    const int g = o / D, d = o - g * D;
+    float M = -INFINITY;
+    for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, base[((long long)s * G + g) * (D + 2) + D]);
+    float num = 0.0f, den = 0.0f;
+    for (int s = 0; s < a.nsplit; ++s) {
+      const float *pp = base + ((long long)s * G + g) * (D + 2);
+      const float ms = pp[D];
+      const float wgt = ms == -INFINITY ? 0.0f : expf(ms - M);
+      num = fmaf(wgt, pp[d], num);
+      den = fmaf(wgt, pp[D + 1], den);
+    }
+    char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)(h * G + g) * D) * ES;
+    store_f32<DT>(ob, d, __fdiv_rn(num, den));
+  }
+}
+
+template <int DT, int D>
+void launch_decode_attn(const DecodeAttnArgs &a, int B, hipStream_t s) {
+  hipLaunchKernelGGL((k_decode_attn<DT, D>), dim3(a.nsplit, a.Hkv, B), dim3(256), 0, s, a);
+  if (a.nsplit > 1) hipLaunchKernelGGL((k_decode_attn_combine<DT, D>), dim3(a.Hkv, B), dim3(256), 0, s, a);
+}
+
 template <int DT, bool ADD>
 void launch_rmsnorm(bool vec, long long rows, const void *x, const void *r, int K, long long ldx, const void *w,
                     float eps, void *y, void *sum, long long ldy, hipStream_t s) {
@@ -230,6 +467,40 @@ extern "C" int qz_silu_mul(const void *gate, const void *up, int dtype, long lon
     case QZ_DT_F16: hipLaunchKernelGGL((k_silu_mul<QZ_DT_F16>), grid, blk, 0, s, gate, up, n, y); break;
     case QZ_DT_BF16: hipLaunchKernelGGL((k_silu_mul<QZ_DT_BF16>), grid, blk, 0, s, gate, up, n, y); break;
     case QZ_DT_F32: hipLaunchKernelGGL((k_silu_mul<QZ_DT_F32>), grid, blk, 0, s, gate, up, n, y); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const void *q, long long q_row,
+                                   const void *k, long long k_row, const void *v, long long v_row, const void *cos,
+                                   const void *sin, long long cs_row, void *k_cache, void *v_cache,
+                                   const void *mask, long long mask_b, long long mask_j, long long *pos,
+                                   unsigned int *arrive, void *out, long long out_row, float *work, float scale,
+                                   void *stream) {
+  if (B < 0 || Hq < 0 || Hkv < 0 || D < 0 || L < 0) return QZ_ERR_ARG;
+  if (B == 0 || Hq == 0) return 0;
+  if (Hkv == 0 || Hq % Hkv != 0 || Hq / Hkv > kAttnMaxG || (D != 64 && D != 128) || L == 0) return QZ_ERR_SHAPE;
+  if (B > 65535 || Hkv > 65535) return QZ_ERR_SHAPE;
+  if (!q || !k || !v || !cos || !sin || !k_cache || !v_cache || !mask || !pos || !arrive || !out) return QZ_ERR_ARG;
+  if (q_row < (long long)Hq * D || k_row < (long long)Hkv * D || v_row < (long long)Hkv * D || cs_row < 0 ||
+      out_row < (long long)Hq * D)
+    return QZ_ERR_ARG;
+  // 16-B row loads of the caches; 4-B words of v
+  if (((uintptr_t)k_cache | (uintptr_t)v_cache) % 16 != 0 || ((uintptr_t)v % 4) != 0 || (v_row % 2) != 0)
+    return QZ_ERR_ARG;
+  DecodeAttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.qs = q_row; a.ks = k_row; a.vs = v_row;
+  a.cos = cos; a.sin = sin; a.cs = cs_row;
+  a.kc = k_cache; a.vc = v_cache;
+  a.mask = reinterpret_cast<const unsigned char *>(mask); a.mb = mask_b; a.mj = mask_j;
+  a.pos = pos; a.arrive = arrive; a.out = out; a.os = out_row; a.part = work;
+  a.Hkv = Hkv; a.G = Hq / Hkv; a.L = L; a.nsplit = (L + kAttnChunk - 1) / kAttnChunk; a.scale = scale;
+  if (a.nsplit > 1 && !work) return QZ_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case QZ_DT_F16: D == 64 ? launch_decode_attn<QZ_DT_F16, 64>(a, B, s) : launch_decode_attn<QZ_DT_F16, 128>(a, B, s); break;
+    case QZ_DT_BF16: D == 64 ? launch_decode_attn<QZ_DT_BF16, 64>(a, B, s) : launch_decode_attn<QZ_DT_BF16, 128>(a, B, s); break;
     default: return QZ_ERR_DTYPE;
   }
   return (int)hipGetLastError();

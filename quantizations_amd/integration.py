@@ -241,6 +241,54 @@ def _fused_mlp_forward(mod: nn.Module):
     return forward
 
 
+def _static_layer(cache, idx):
+    """The StaticLayer (cache_utils.py:400-487) holding layer `idx` of a StaticCache, or None."""
+    layers = getattr(cache, "layers", None)
+    if layers is None or idx is None or idx >= len(layers):
+        return None
+    layer = layers[idx]
+    if type(layer).__name__ != "StaticLayer" or not getattr(layer, "is_initialized", False):
+        return None
+    return layer
+
+
+def _fused_attention_forward(mod: nn.Module, orig):
+    """LlamaAttention.forward (modeling_llama.py:243-281) with everything between the q/k/v
+    projections and o_proj as ONE launch (layer_ops.decode_attention) when a single new token
+    meets a StaticCache layer and the bool mask sdpa would get; any other call (prefill, other
+    caches, eager/flash attention, float masks) runs the original forward."""
+    from .layer_ops import decode_attention, decode_attention_supported
+
+    def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None, **kwargs):
+        layer = None
+        if (hidden_states.dim() == 3 and hidden_states.shape[1] == 1 and position_embeddings is not None
+                and not kwargs.get("output_attentions", False) and not mod.training
+                and getattr(mod.config, "_attn_implementation", None) == "sdpa"):
+            layer = _static_layer(past_key_values, getattr(mod, "layer_idx", None))
+        if layer is not None:
+            cos, sin = position_embeddings
+            # query heads of THIS module: the cache holds its kv heads (a tensor-parallel rank
+            # keeps a share of them), the GQA ratio is the model's
+            nq = layer.keys.shape[1] * (mod.config.num_attention_heads // mod.config.num_key_value_heads) \
+                if layer.keys.dim() == 4 else 0
+            if layer.keys.shape[-1] == mod.head_dim and decode_attention_supported(
+                    hidden_states, cos, layer.keys, layer.values, attention_mask, layer.cumulative_length, nq):
+                arrive = mod.__dict__.get("_qz_attn_arrive")
+                if arrive is None or arrive.device != hidden_states.device:
+                    arrive = torch.zeros(1, dtype=torch.int32, device=hidden_states.device)
+                    mod.__dict__["_qz_attn_arrive"] = arrive
+                q = mod.q_proj(hidden_states)
+                k = mod.k_proj(hidden_states)
+                v = mod.v_proj(hidden_states)
+                if q.shape[-1] != nq * mod.head_dim or k.shape[-1] != layer.keys.shape[1] * mod.head_dim:
+                    return orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+                out = decode_attention(q, k, v, cos, sin, layer.keys, layer.values, attention_mask,
+                                       layer.cumulative_length, arrive, nq, mod.scaling)
+                return mod.o_proj(out), None
+        return orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+    return forward
+
+
 def _fused_decoder_forward(mod: nn.Module):
     """LlamaDecoderLayer.forward (modeling_llama.py:295-324) with lines 317-321
     (`residual + h`, then post_attention_layernorm) as one add_rms_norm launch."""
@@ -266,7 +314,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
-                   decoder: bool = False) -> int:
+                   decoder: bool = False, attention: bool = True) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -275,7 +323,10 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     take keep the original code.  Returns the number of modules patched (norms,
     MLPs, decoder layers, and modeling modules whose apply_rotary_pos_emb was
     replaced).  `decoder` (opt-in) replaces LlamaDecoderLayer.forward itself with
-    a restatement; it measured no gain on the bs=1 graph step."""
+    a restatement; it measured no gain on the bs=1 graph step.
+    `attention` routes a decode step's rotary + StaticCache update + sdpa attention of
+    each Llama/Mistral/Qwen2 attention module through layer_ops.decode_attention (counted
+    once per module)."""
     import sys
 
     n = 0
@@ -297,7 +348,14 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
             m.__dict__["forward"] = _fused_mlp_forward(m)
             m.__dict__["_qz_fused_mlp"] = True
             n += 1
-        elif rope and name in ATTENTION_CLASSES:
+        elif (rope or attention) and name in ATTENTION_CLASSES:
+            if attention and "forward" not in m.__dict__ and all(
+                    hasattr(m, a) for a in ("q_proj", "k_proj", "v_proj", "o_proj", "scaling", "head_dim")):
+                m.__dict__["forward"] = _fused_attention_forward(m, m.forward)
+                m.__dict__["_qz_fused_attn"] = True
+                n += 1
+            if not rope:
+                continue
             modname = type(m).__module__
             mod = sys.modules.get(modname)
             fn = getattr(mod, "apply_rotary_pos_emb", None)
@@ -316,8 +374,9 @@ def unfuse_layer_ops(model: nn.Module) -> None:
     unfuse_prenorm(model)
     for m in model.modules():
         if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None) or \
-                m.__dict__.pop("_qz_fused_decoder", None):
+                m.__dict__.pop("_qz_fused_decoder", None) or m.__dict__.pop("_qz_fused_attn", None):
             m.__dict__.pop("forward", None)
+            m.__dict__.pop("_qz_attn_arrive", None)
     for modname, fn in list(_ROPE_PATCHED.items()):
         setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)
         del _ROPE_PATCHED[modname]

@@ -122,3 +122,70 @@ def silu_mul(g: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
     _lib.check(_lib.lib.qz_silu_mul(g.data_ptr(), u.data_ptr(), _lib.dtype_code(g.dtype), g.numel(), y.data_ptr(),
                                     _lib.stream_of(g)), "qz_silu_mul")
     return y
+
+
+ATTN_CHUNK = 128  # key positions per workgroup of qz_decode_attention (csrc/layer_ops.hip)
+
+
+def decode_attention_supported(q: torch.Tensor, cos: torch.Tensor, key_cache: torch.Tensor,
+                               value_cache: torch.Tensor, mask, pos, num_heads: int) -> bool:
+    """What qz_decode_attention takes: one new token per sequence (q, or the layer input:
+    [B, 1, *]), 16-bit activations, a contiguous static cache [B, Hkv, L, D] with D in {64, 128}
+    and Hq/Hkv <= 8, a bool mask [B or 1, 1, 1, L], cos/sin [B or 1, 1, D] and an int64 position
+    on the GPU.  Metadata only: nothing is launched or allocated."""
+    if not (q.is_cuda and q.dtype in (torch.float16, torch.bfloat16) and q.dim() == 3 and q.shape[1] == 1):
+        return False
+    if key_cache.dim() != 4 or value_cache.shape != key_cache.shape:
+        return False
+    B, Hkv, L, D = key_cache.shape
+    if D not in (64, 128) or num_heads % Hkv or num_heads // Hkv > 8 or q.shape[0] != B or L == 0:
+        return False
+    for t in (key_cache, value_cache):
+        if t.dtype != q.dtype or t.device != q.device or not t.is_contiguous() or t.data_ptr() % 16:
+            return False
+    if not (isinstance(mask, torch.Tensor) and mask.dtype == torch.bool and mask.device == q.device
+            and mask.dim() == 4 and mask.shape[0] in (1, B) and mask.shape[1] == 1 and mask.shape[2] == 1
+            and mask.shape[3] == L):
+        return False
+    if not (cos.dim() == 3 and cos.shape[0] in (1, B) and cos.shape[1] == 1 and cos.shape[2] == D
+            and cos.dtype == q.dtype and cos.device == q.device and cos.stride(-1) == 1):
+        return False
+    return (isinstance(pos, torch.Tensor) and pos.dtype == torch.int64 and pos.numel() == 1 and pos.device == q.device)
+
+
+def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                     key_cache: torch.Tensor, value_cache: torch.Tensor, mask: torch.Tensor, pos: torch.Tensor,
+                     arrive: torch.Tensor, num_heads: int, scale: float) -> torch.Tensor:
+    """LlamaAttention.forward for one new token per sequence against a static cache, up to the
+    o_proj input: rotary of q/k, key_cache/value_cache[:, :, pos] = k, v, pos += 1 (all on the
+    GPU, graph-capturable), masked GQA softmax(q k^T * scale) v.  q [B, 1, Hq*D], k/v
+    [B, 1, Hkv*D] (the projection outputs), cos/sin [B or 1, 1, D], caches [B, Hkv, L, D],
+    mask bool [B or 1, 1, 1, L], pos int64 (StaticLayer.cumulative_length), arrive a zeroed
+    int32 scratch word.  Returns [B, 1, Hq*D]."""
+    if not decode_attention_supported(q, cos, key_cache, value_cache, mask, pos, num_heads):
+        raise ValueError("decode_attention: unsupported shapes/dtypes/layout")
+    B, Hkv, L, D = key_cache.shape
+    G = num_heads // Hkv
+    if q.shape[2] != num_heads * D:
+        raise ValueError("decode_attention: q width differs from num_heads * head_dim")
+    if sin.shape != cos.shape or sin.stride() != cos.stride() or sin.dtype != cos.dtype:
+        raise ValueError("decode_attention: sin must match cos")
+    q2, k2, v2 = (t.reshape(B, -1) for t in (q, k, v))
+    k2 = k2 if k2.stride(-1) == 1 else k2.contiguous()
+    q2 = q2 if q2.stride(-1) == 1 else q2.contiguous()
+    if v2.stride(-1) != 1 or v2.stride(0) % 2 or v2.data_ptr() % 4:
+        v2 = v2.contiguous()
+    if k2.shape[1] != Hkv * D or v2.shape[1] != Hkv * D:
+        raise ValueError("decode_attention: k/v width differs from the cache's heads")
+    out = torch.empty((B, 1, num_heads * D), dtype=q.dtype, device=q.device)
+    nsplit = -(-L // ATTN_CHUNK)
+    work = torch.empty(B * Hkv * nsplit * G * (D + 2), dtype=torch.float32, device=q.device) if nsplit > 1 else None
+    cs_row = cos.stride(0) if cos.shape[0] == B and B > 1 else 0
+    mb = mask.stride(0) if mask.shape[0] == B and B > 1 else 0
+    _lib.check(_lib.lib.qz_decode_attention(
+        _lib.dtype_code(q.dtype), B, num_heads, Hkv, D, L, q2.data_ptr(), q2.stride(0), k2.data_ptr(), k2.stride(0),
+        v2.data_ptr(), v2.stride(0), cos.data_ptr(), sin.data_ptr(), cs_row, key_cache.data_ptr(),
+        value_cache.data_ptr(), mask.data_ptr(), mb, mask.stride(3), pos.data_ptr(), arrive.data_ptr(),
+        out.data_ptr(), num_heads * D, work.data_ptr() if work is not None else None, float(scale),
+        _lib.stream_of(q)), "qz_decode_attention")
+    return out

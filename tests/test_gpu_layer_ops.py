@@ -196,7 +196,8 @@ def test_tiny_llama_fuse_layer_ops_decode_and_graph():
         ref_toks, ref_logits = greedy(6)
         ref_graph = graph_logits(ref_toks[:, :1])
         n = fuse_layer_ops(model, decoder=True)
-        assert n == 4 * cfg.num_hidden_layers + 1 + 1  # 2 norms + MLP + decoder layer each, final norm, rope
+        # 2 norms + MLP + decoder layer + attention module each, final norm, rope
+        assert n == 5 * cfg.num_hidden_layers + 1 + 1
         toks, logits = greedy(6)
         assert torch.equal(toks, ref_toks)
         for a, b in zip(logits, ref_logits):

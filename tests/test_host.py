@@ -98,6 +98,7 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     do not apply and transformers' own code runs, so logits are unchanged; unfuse
     restores the original forwards and apply_rotary_pos_emb."""
     from transformers import LlamaConfig, LlamaForCausalLM
+    from transformers.cache_utils import StaticCache
     import transformers.models.llama.modeling_llama as ml
 
     from quantizations_amd.integration import fuse_layer_ops, unfuse_layer_ops
@@ -111,10 +112,21 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     orig = ml.apply_rotary_pos_emb
     with torch.no_grad():
         ref = model(input_ids=ids).logits
-        assert fuse_layer_ops(model, decoder=True) == 2 * 2 + 1 + 2 + 2 + 1  # norms, final norm, MLPs, decoder layers, rope
+        cache = StaticCache(config=cfg, max_cache_len=8)
+        ref_pre = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(5)).logits
+        p5 = torch.tensor([5])
+        ref_step = model(input_ids=ids[:, :1], past_key_values=cache, cache_position=p5,
+                         position_ids=p5.view(1, 1)).logits
+        # norms, final norm, MLPs, decoder layers, attention modules, rope
+        assert fuse_layer_ops(model, decoder=True) == 2 * 2 + 1 + 2 + 2 + 2 + 1
+        cache = StaticCache(config=cfg, max_cache_len=8)     # CPU decode: the attention patch defers
+        pre = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(5)).logits
+        p5 = torch.tensor([5])
+        step = model(input_ids=ids[:, :1], past_key_values=cache, cache_position=p5, position_ids=p5.view(1, 1)).logits
         assert ml.apply_rotary_pos_emb is not orig and ml.apply_rotary_pos_emb._qz_orig is orig
         assert fuse_layer_ops(model) == 0  # idempotent
         assert torch.equal(model(input_ids=ids).logits, ref)
+        assert torch.equal(pre, ref_pre) and torch.equal(step, ref_step)
         unfuse_layer_ops(model)
     assert ml.apply_rotary_pos_emb is orig
     assert not any("forward" in m.__dict__ for m in model.modules())

@@ -180,11 +180,12 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
-                         prenorm: bool = True):
+                         prenorm: bool = True, attention: bool = True, residual: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
-    groups and the one-launch layer ops, and (single-GPU layout, `prenorm`) absorb
+    groups and the one-launch layer ops (with `attention`, the decode step's rotary + cache
+    update + attention as one launch), and (single-GPU layout, `prenorm`) absorb
     each layer's two RMSNorms into those groups' launches.  `local_matmul` is the CPU
     test hook of parallel.py (None = the HIP kernels).  Returns (n_groups,
     n_layer_ops); absorbed norms count as layer ops."""
@@ -209,7 +210,9 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
         n_layer_ops = fuse_layer_ops(model, norm=layer_ops in ("all", "all+decoder", "norm"),
                                      rope=layer_ops in ("all", "all+decoder", "rope"),
                                      mlp=layer_ops in ("all", "all+decoder", "mlp"),
-                                     decoder=layer_ops == "all+decoder")  # one HIP launch each
+                                     decoder=layer_ops == "all+decoder",
+                                     attention=attention and layer_ops in ("all", "all+decoder"),
+                                     residual=residual)  # one launch each
     if prenorm and fuse and not sharded and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -870,6 +873,12 @@ def main():
     ap.add_argument("--no-prenorm", action="store_true",
                     help="keep each RMSNorm as its own launch (default: absorbed into the q/k/v and gate/up "
                          "grouped GEMV launches on one GPU)")
+    ap.add_argument("--no-attention", action="store_true",
+                    help="keep transformers' rotary + StaticCache update + sdpa (14 launches per layer) instead of "
+                         "the one-launch layer_ops.decode_attention")
+    ap.add_argument("--no-residual", action="store_true",
+                    help="keep each decoder layer's two residual adds as their own launches (default: in the "
+                         "o_proj / down_proj GEMV epilogues)")
     ap.add_argument("--layer-ops", choices=("all", "all+decoder", "norm", "rope", "mlp", "none"), default="all",
                     help="which transformers ops integration.fuse_layer_ops replaces")
     ap.add_argument("--capture-mode", choices=("global", "thread_local", "relaxed"), default="thread_local",
@@ -963,7 +972,9 @@ def main():
                                  compute_dtype=cdt)
         n_groups, n_layer_ops = prepare_decode_model(model, rank, world, sharded, tp_mode, fuse=not args.no_fuse,
                                                      layer_ops=layer_ops, gatherer=gatherer,
-                                                     prenorm=not args.no_prenorm)
+                                                     prenorm=not args.no_prenorm,
+                                                     attention=not args.no_attention,
+                                                     residual=not args.no_residual)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1089,6 +1100,10 @@ def main():
         line["config"]["compute_dtype"] = args.compute_dtype
         line["config"]["rmsnorm_in_grouped_gemv"] = bool(not args.no_prenorm and not sharded and not args.no_fuse
                                                          and layer_ops in ("all", "norm"))
+        line["config"]["decode_attention"] = ("qz_decode_attention" if not args.no_attention
+                                              and layer_ops in ("all", "all+decoder") else "transformers sdpa")
+        line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
+                                                           and layer_ops == "all")
         if exchange is not None:
             line["config"]["exchange"] = exchange
         if extra_codes is not None:

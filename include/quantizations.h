@@ -118,6 +118,15 @@ int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B,
                  const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
                  void *y, void *stream);
 
+/* qz_gemv_4bit with a residual add in the epilogue -- LlamaDecoderLayer.forward's
+ * `residual + h` (modeling_llama.py:316,322) on the o_proj / down_proj output:
+ *   y[r] = round(residual[r] + round(gemv[r]))   (both roundings to `dtype`, as torch stores h
+ * and then the sum), residual [M] of `dtype`.  One launch instead of two. */
+int qz_gemv_4bit_residual(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
+                          int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
+                          const float *code2, const float *offset, int blocksize2, long long block_base,
+                          const float *lut, const void *bias, const void *residual, void *y, void *stream);
+
 /* Grouped decode GEMV: several Linear4bit layers that
  * read the SAME x (q/k/v, or gate/up, of one decoder layer) in ONE launch,
  * replacing nseg separate modules.py:56-61 calls.  Each segment keeps its own

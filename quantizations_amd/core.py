@@ -410,12 +410,14 @@ def exact_codes_for(compute_dtype):
 
 def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=False, transposed_B=False,
               state=None, bias: Optional[Tensor] = None, block_base: int = 0,
-              exact_codes: Optional[bool] = None) -> Tensor:
+              exact_codes: Optional[bool] = None, residual: Optional[Tensor] = None) -> Tensor:
     """Batch-1 4-bit GEMV (reference core.py:426-504) as ONE fused kernel:
     y = x . W^T (+ bias), W from `state`; out dtype = A.dtype.  fp32 activations are
     multiplied by the fp32 codebook values and bf16 ones by bf16 hi + lo codes; for fp16
     activations `exact_codes` (default GEMV_EXACT_CODES) picks the exact hi + lo fp16 codes
-    over the fp16-rounded ones."""
+    over the fp16-rounded ones.  `residual` (a contiguous A.dtype tensor of M elements;
+    not in the reference): returns residual + y with the add in the kernel's epilogue
+    (qz_gemv_4bit_residual, bit-identical to the torch add)."""
     if state is None:
         raise ValueError("state cannot None. gem_4bit( ) requires the state from quantize_4bit( )")
     if A.numel() != A.shape[-1]:
@@ -430,6 +432,15 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     A = A.contiguous()
     if bias is not None and bias.dtype != A.dtype:
         bias = bias.to(A.dtype)
+    if residual is not None:
+        if residual.dtype != A.dtype or residual.numel() != M or not residual.is_contiguous() \
+                or residual.device != A.device:
+            raise ValueError(f"gemv_4bit: residual must be a contiguous {A.dtype} tensor of {M} elements")
+        check(lib.qz_gemv_4bit_residual(M, K, ptr(A), dtype_code(A.dtype), ptr(B),
+                                        _gemv_quant_type(state.quant_type, exact_codes, A.dtype), state.blocksize,
+                                        *state.scale_args(), block_base, 0, ptr(bias), ptr(residual), ptr(out),
+                                        _lib.stream_of(A)), "gemv_4bit(residual)")
+        return out
     check(lib.qz_gemv_4bit(M, K, ptr(A), dtype_code(A.dtype), ptr(B), _gemv_quant_type(state.quant_type, exact_codes, A.dtype),
                            state.blocksize, *state.scale_args(), block_base, 0, ptr(bias), ptr(out),
                            _lib.stream_of(A)), "gemv_4bit")

@@ -186,6 +186,18 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
+// v rounded to the storage format of DT (the conversions store_f32 uses), back as fp32
+template <int DT> __device__ __forceinline__ float round_store(float v) {
+  if constexpr (DT == QZ_DT_F16) return __half2float(__ushort_as_half(f32_to_f16_bits(v)));
+  else if constexpr (DT == QZ_DT_BF16) return __bfloat162float(__float2bfloat16(v));
+  else return v;
+}
+// LlamaDecoderLayer's `residual + h` on the projection output h as torch stores it (rounded), the
+// sum rounded again by the store
+template <int DT> __device__ __forceinline__ float add_res(float o, const void *res, long long row) {
+  return res ? __fadd_rn(load_f32<DT>(res, row), round_store<DT>(o)) : o;
+}
+
 // two outputs in the 16-bit format of DT, element 0 in the low half (each converted exactly as
 // store_f32 converts it)
 template <int DT> __device__ __forceinline__ uint32_t pack16(float a, float b) {
@@ -213,6 +225,7 @@ struct GemvParams {
   uint32_t tab[8];
   const void *nw;    // fused pre-norm (NRM): the RMSNorm weight [K], or nullptr
   float eps;         //   and its epsilon
+  const void *res;   // residual [M] added after the output rounding (y = round(round(x W^T) + res)), or nullptr
 };
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -302,6 +315,7 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   p.bs2_log2 = keep_s(in.bs2_log2);
   p.out_scale = keep_s(in.out_scale);
   p.tabsel = keep_s(in.tabsel);
+  p.res = keep_sp(in.res);
 #pragma unroll
   for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
   p.nw = keep_sp(in.nw);
@@ -1088,6 +1102,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
             o0 += load_f32<DT>(p.bias, row0 + r);
             o1 += load_f32<DT>(p.bias, row0 + r + 1);
           }
+          o0 = add_res<DT>(o0, p.res, row0 + r);
+          o1 = add_res<DT>(o1, p.res, row0 + r + 1);
           reinterpret_cast<uint32_t *>(p.y)[(row0 + r) >> 1] = pack16<DT>(o0, o1);
         }
       } else {
@@ -1097,6 +1113,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
           if (row < p.M) {
             float o = v[r] * out_scale;
             if (p.bias) o += load_f32<DT>(p.bias, row);
+            o = add_res<DT>(o, p.res, row);
             if constexpr ((ABL & 1024) != 0 && DT == QZ_DT_F16)  // microbenchmark: non-temporal y store
               __builtin_nontemporal_store((uint16_t)f32_to_f16_bits(o), reinterpret_cast<uint16_t *>(p.y) + row);
             else
@@ -1124,7 +1141,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       for (int k = 0; k < WK; ++k) v += s_part[g * WK + k][r];
       v *= out_scale;
       if (p.bias) v += load_f32<DT>(p.bias, row);
-      store_f32<DT>(p.y, row, v);
+      store_f32<DT>(p.y, row, add_res<DT>(v, p.res, row));
     }
   }
 }
@@ -1301,7 +1318,7 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_generic(GemvParams p, int qua
   acc = wave_sum_last(acc);
   if (lane == kWave - 1) {
     if (p.bias) acc += load_f32<DT>(p.bias, row);
-    store_f32<DT>(p.y, row, acc);
+    store_f32<DT>(p.y, row, add_res<DT>(acc, p.res, row));
   }
 }
 
@@ -1480,6 +1497,7 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   p->bs2_log2 = bs2l;
   p->nw = nullptr;
   p->eps = 0.0f;
+  p->res = nullptr;
   *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
             (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
             (long long)M * K + 2LL * 1024 < (1LL << 32) &&            // 32-bit element offsets
@@ -1487,15 +1505,16 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   return QZ_OK;
 }
 
-extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
-                            int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
-                            const float *code2, const float *offset, int blocksize2, long long block_base,
-                            const float *lut, const void *bias, void *y, void *stream) {
+static int gemv_impl(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type, int blocksize,
+                     const float *absmax, const unsigned char *qabsmax, const float *absmax2, const float *code2,
+                     const float *offset, int blocksize2, long long block_base, const float *lut, const void *bias,
+                     const void *res, void *y, void *stream) {
   GemvParams p;
   bool vec_ok;
   const int st = make_params(M, K, x, dtype, B, quant_type, blocksize, absmax, qabsmax, absmax2, code2, offset,
                              blocksize2, block_base, lut, bias, y, &p, &vec_ok);
   if (st != QZ_OK) return st;
+  p.res = res;
   if (M == 0) return QZ_OK;
   const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
@@ -1527,6 +1546,24 @@ extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsign
   if (rc != QZ_OK) return rc;
   QZ_LAUNCH_CHECK();
   return QZ_OK;
+}
+
+extern "C" int qz_gemv_4bit(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
+                            int blocksize, const float *absmax, const unsigned char *qabsmax, const float *absmax2,
+                            const float *code2, const float *offset, int blocksize2, long long block_base,
+                            const float *lut, const void *bias, void *y, void *stream) {
+  return gemv_impl(M, K, x, dtype, B, quant_type, blocksize, absmax, qabsmax, absmax2, code2, offset, blocksize2,
+                   block_base, lut, bias, nullptr, y, stream);
+}
+
+extern "C" int qz_gemv_4bit_residual(int M, int K, const void *x, int dtype, const unsigned char *B, int quant_type,
+                                     int blocksize, const float *absmax, const unsigned char *qabsmax,
+                                     const float *absmax2, const float *code2, const float *offset, int blocksize2,
+                                     long long block_base, const float *lut, const void *bias, const void *residual,
+                                     void *y, void *stream) {
+  if (!residual) return QZ_ERR_ARG;
+  return gemv_impl(M, K, x, dtype, B, quant_type, blocksize, absmax, qabsmax, absmax2, code2, offset, blocksize2,
+                   block_base, lut, bias, residual, y, stream);
 }
 
 // nw != nullptr: x is first RMSNorm'd with weight nw / epsilon eps, bit-identically to qz_rmsnorm

@@ -233,11 +233,28 @@ def _fused_rope(orig):
 def _fused_mlp_forward(mod: nn.Module):
     from .layer_ops import silu_mul, silu_mul_supported
 
-    def forward(x: torch.Tensor) -> torch.Tensor:
+    def forward(x: torch.Tensor, _qz_residual=None) -> torch.Tensor:
         g = mod.gate_proj(x)  # same call order as LlamaMLP.forward (a DecodeGroup launches gate+up here)
         u = mod.up_proj(x)
         h = silu_mul(g, u) if silu_mul_supported(g, u) else mod.act_fn(g) * u
-        return mod.down_proj(h)
+        return _project(mod.down_proj, h, _qz_residual)
+    return forward
+
+
+def _residual_decoder_forward(mod: nn.Module):
+    """LlamaDecoderLayer.forward (modeling_llama.py:295-324) with both `residual + h` adds
+    moved into the epilogues of the o_proj and down_proj GEMVs (their modules were patched by
+    fuse_layer_ops and take `_qz_residual`); the norms are called as the model has them (an
+    identity once fuse_prenorm absorbed them).  Bit-identical to the original."""
+    def forward(hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
+                position_embeddings=None, **kwargs):
+        h = mod.input_layernorm(hidden_states)
+        hidden_states, _ = mod.self_attn(hidden_states=h, attention_mask=attention_mask, position_ids=position_ids,
+                                         past_key_values=past_key_values, use_cache=use_cache,
+                                         position_embeddings=position_embeddings, _qz_residual=hidden_states,
+                                         **kwargs)
+        h = mod.post_attention_layernorm(hidden_states)
+        return mod.mlp(h, _qz_residual=hidden_states)
     return forward
 
 
@@ -259,7 +276,9 @@ def _fused_attention_forward(mod: nn.Module, orig):
     caches, eager/flash attention, float masks) runs the original forward."""
     from .layer_ops import decode_attention, decode_attention_supported
 
-    def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None, **kwargs):
+    def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None,
+                _qz_residual=None, **kwargs):
+        # _qz_residual (the residual-fused decoder layer): return residual + attention output
         layer = None
         if (hidden_states.dim() == 3 and hidden_states.shape[1] == 1 and position_embeddings is not None
                 and not kwargs.get("output_attentions", False) and not mod.training
@@ -284,9 +303,19 @@ def _fused_attention_forward(mod: nn.Module, orig):
                     return orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
                 out = decode_attention(q, k, v, cos, sin, layer.keys, layer.values, attention_mask,
                                        layer.cumulative_length, arrive, nq, mod.scaling)
-                return mod.o_proj(out), None
-        return orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+                return _project(mod.o_proj, out, _qz_residual), None
+        h, w = orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+        return (h if _qz_residual is None else _qz_residual + h), w
     return forward
+
+
+def _project(proj: nn.Module, x: torch.Tensor, residual):
+    """proj(x), or residual + proj(x) with the add in the GEMV epilogue where proj is a
+    Linear4bit that decodes x on its own (Linear4bit.forward_residual)."""
+    if residual is None:
+        return proj(x)
+    fr = getattr(proj, "forward_residual", None)
+    return fr(x, residual) if fr is not None else residual + proj(x)
 
 
 def _fused_decoder_forward(mod: nn.Module):
@@ -314,7 +343,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
-                   decoder: bool = False, attention: bool = True) -> int:
+                   decoder: bool = False, attention: bool = True, residual: bool = True) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -326,7 +355,8 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     a restatement; it measured no gain on the bs=1 graph step.
     `attention` routes a decode step's rotary + StaticCache update + sdpa attention of
     each Llama/Mistral/Qwen2 attention module through layer_ops.decode_attention (counted
-    once per module)."""
+    once per module).  `residual` (with `attention` and `mlp`) moves each decoder layer's two
+    residual adds into the o_proj / down_proj GEMV epilogues (counted once per layer)."""
     import sys
 
     n = 0
@@ -363,6 +393,14 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
                 _ROPE_PATCHED[modname] = fn
                 mod.apply_rotary_pos_emb = _fused_rope(fn)
                 n += 1
+    if residual and attention and mlp and not decoder:
+        for m in model.modules():
+            if type(m).__name__ in DECODER_CLASSES and "forward" not in m.__dict__ and \
+                    "_qz_fused_attn" in getattr(m, "self_attn", nn.Module()).__dict__ and \
+                    "_qz_fused_mlp" in getattr(m, "mlp", nn.Module()).__dict__:
+                m.__dict__["forward"] = _residual_decoder_forward(m)
+                m.__dict__["_qz_residual_decoder"] = True
+                n += 1
     return n
 
 
@@ -374,7 +412,8 @@ def unfuse_layer_ops(model: nn.Module) -> None:
     unfuse_prenorm(model)
     for m in model.modules():
         if m.__dict__.pop("_qz_fused_norm", None) or m.__dict__.pop("_qz_fused_mlp", None) or \
-                m.__dict__.pop("_qz_fused_decoder", None) or m.__dict__.pop("_qz_fused_attn", None):
+                m.__dict__.pop("_qz_fused_decoder", None) or m.__dict__.pop("_qz_fused_attn", None) or \
+                m.__dict__.pop("_qz_residual_decoder", None):
             m.__dict__.pop("forward", None)
             m.__dict__.pop("_qz_attn_arrive", None)
     for modname, fn in list(_ROPE_PATCHED.items()):

@@ -148,6 +148,23 @@ class Linear4bit(nn.Linear):
                           exact_codes=exact_codes_for(self.compute_dtype))
         return out if out.dtype == inp_dtype else out.to(inp_dtype)
 
+    def forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """residual + self(x) -- LlamaDecoderLayer's `residual + h` after o_proj / down_proj --
+        with the add in the decode GEMV's epilogue (one launch, bit-identical to the torch
+        add) when x is a single token this layer decodes on its own; otherwise the two ops."""
+        qs = self.weight.quant_state
+        if (qs is not None and x.is_cuda and x.numel() == x.shape[-1] and self.__dict__.get("_qz_group") is None
+                and residual.dtype == x.dtype and residual.device == x.device and residual.is_contiguous()
+                and residual.numel() == qs.shape[0] and residual.shape[:-1] == x.shape[:-1]):
+            if not self.compute_type_is_set:
+                self.set_compute_type(x)
+                self.compute_type_is_set = True
+            if self._input(x) is x:
+                bias = None if self.bias is None else self.bias.to(x.dtype)
+                return gemv_4bit(x, self.weight, state=qs, bias=bias, exact_codes=exact_codes_for(self.compute_dtype),
+                                 residual=residual)
+        return residual + self(x)
+
     # -- checkpoints: bnb-compatible keys (QuantState.as_dict(packed=True)) --
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         super()._save_to_state_dict(destination, prefix, keep_vars)

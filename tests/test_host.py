@@ -136,6 +136,40 @@ def test_fuse_layer_ops_patches_and_restores_on_cpu():
     assert not rope_supported(q, q, torch.randn(1, 3, 16), torch.randn(1, 3, 16))
 
 
+def test_fuse_layer_ops_residual_decoder_on_cpu_is_bit_identical():
+    """The default fuse_layer_ops also restates each decoder layer so that its two residual
+    adds can run in the o_proj / down_proj epilogues; on CPU (no kernels) every patched
+    forward defers to torch in the original operand order: logits of prefill and of a
+    StaticCache decode step are bit-identical, and unfuse removes every patch."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from transformers.cache_utils import StaticCache
+
+    from quantizations_amd.integration import fuse_layer_ops, unfuse_layer_ops
+
+    cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=97)
+    torch.manual_seed(1)
+    model = LlamaForCausalLM(cfg).eval()
+    ids = torch.randint(0, 97, (1, 5))
+
+    def run():
+        cache = StaticCache(config=cfg, max_cache_len=8)
+        a = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(5)).logits
+        p5 = torch.tensor([5])
+        b = model(input_ids=ids[:, :1], past_key_values=cache, cache_position=p5, position_ids=p5.view(1, 1)).logits
+        return a, b
+
+    with torch.no_grad():
+        ref = run()
+        # norms + final norm, MLPs, attention modules, rope, residual decoder layers
+        assert fuse_layer_ops(model) == 2 * 2 + 1 + 2 + 2 + 1 + 2
+        assert sum("_qz_residual_decoder" in m.__dict__ for m in model.modules()) == 2
+        got = run()
+        assert all(torch.equal(x, y) for x, y in zip(got, ref))
+        unfuse_layer_ops(model)
+    assert not any(k.startswith("_qz") or k == "forward" for m in model.modules() for k in m.__dict__)
+
+
 def test_fuse_prenorm_absorbs_only_cuda_norms_of_plain_groups():
     """fuse_prenorm needs a Linear4bit decode group (not a row-sharded one) and a norm weight
     on the GPU: on a CPU model it absorbs nothing; a group whose compute is not the Linear4bit

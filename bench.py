@@ -180,7 +180,8 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
-                         prenorm: bool = True, attention: bool = True, residual: bool = True):
+                         prenorm: bool = True, attention: bool = True, residual: bool = True,
+                         mlp_pair: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -212,7 +213,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      mlp=layer_ops in ("all", "all+decoder", "mlp"),
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
-                                     residual=residual)  # one launch each
+                                     residual=residual, mlp_pair=mlp_pair)  # one launch each
     if prenorm and fuse and not sharded and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -876,6 +877,8 @@ def main():
     ap.add_argument("--no-attention", action="store_true",
                     help="keep transformers' rotary + StaticCache update + sdpa (14 launches per layer) instead of "
                          "the one-launch layer_ops.decode_attention")
+    ap.add_argument("--no-mlp-pair", action="store_true",
+                    help="gate/up as the grouped launch + a separate SiLU-product launch (default: one launch)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -974,7 +977,8 @@ def main():
                                                      layer_ops=layer_ops, gatherer=gatherer,
                                                      prenorm=not args.no_prenorm,
                                                      attention=not args.no_attention,
-                                                     residual=not args.no_residual)
+                                                     residual=not args.no_residual,
+                                                     mlp_pair=not args.no_mlp_pair)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1102,6 +1106,8 @@ def main():
                                                          and layer_ops in ("all", "norm"))
         line["config"]["decode_attention"] = ("qz_decode_attention" if not args.no_attention
                                               and layer_ops in ("all", "all+decoder") else "transformers sdpa")
+        line["config"]["silu_in_gate_up_launch"] = bool(not args.no_mlp_pair and not args.no_fuse
+                                                        and layer_ops in ("all", "all+decoder", "mlp"))
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
         if exchange is not None:

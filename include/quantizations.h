@@ -323,6 +323,17 @@ int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const v
                         long long mask_b, long long mask_j, long long *pos, unsigned int *arrive, void *out,
                         long long out_row, float *work, float scale, void *stream);
 
+/* LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) for hidden_act "silu" (modeling_llama.py:175) as
+ * ONE launch: segs[0] = gate_proj, segs[1] = up_proj (equal M; their `y` are ignored), both
+ * GEMVs as qz_gemv_4bit_grouped computes them, then h[r] = round(round(g / (1 + exp(-g))) * u)
+ * on the rounded g[r], u[r] (qz_silu_mul's arithmetic) -- bit-identical to the grouped launch +
+ * qz_silu_mul.  norm_weight (nullable): x is first RMSNorm'd as qz_gemv_4bit_grouped_rmsnorm does.
+ * F16/BF16, full K-steps (K % 2048 == 0), geometries with whole rows per wave; otherwise
+ * QZ_ERR_SHAPE and nothing launched. */
+int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
+                           int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,
+                           void *h, void *stream);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

@@ -447,6 +447,42 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     return out
 
 
+def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> Optional[Tensor]:
+    """F.silu(gate) * up for items = [(B, state, bias)] of gate_proj and up_proj (equal shapes)
+    and a single-token A, in ONE launch (qz_gemv_4bit_pair_silu): bit-identical to
+    gemv_4bit_grouped + layer_ops.silu_mul.  norm=(weight, eps) as in gemv_4bit_grouped.
+    Returns None for what the kernel does not take (the caller runs the two launches)."""
+    items = list(items)
+    if len(items) != 2 or A.numel() != A.shape[-1] or A.dtype not in (torch.float16, torch.bfloat16):
+        return None
+    (B0, s0, b0), (B1, s1, b1) = items
+    K = s0.shape[1]
+    if (A.shape[-1] != K or s1.shape != s0.shape or s1.quant_type != s0.quant_type or s1.blocksize != s0.blocksize
+            or s1.nested != s0.nested or (s0.nested and s1.state2.blocksize != s0.state2.blocksize)):
+        return None
+    A = A.contiguous()
+    M = s0.shape[0]
+    segs = (_lib.GemvSegment * 2)()
+    for i, (B, st, bias) in enumerate(items):
+        if bias is not None and bias.dtype != A.dtype:
+            bias = bias.to(A.dtype)
+        am, qam, am2, code2, off, _ = st.scale_args()
+        segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, 0, ptr(bias), None)
+    shape = (A.shape[0], A.shape[1], M) if A.dim() == 3 else (A.shape[0], M) if A.dim() == 2 else (M,)
+    h = torch.empty(shape, dtype=A.dtype, device=A.device)
+    nw, eps = (None, 0.0) if norm is None else norm
+    if nw is not None and not (nw.dtype == A.dtype and nw.is_cuda and nw.is_contiguous() and nw.numel() == K):
+        return None
+    bs2 = int(s0.state2.blocksize) if s0.nested else 0
+    rc = lib.qz_gemv_4bit_pair_silu(ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
+                                    _gemv_quant_type(s0.quant_type, exact_codes, A.dtype), s0.blocksize, bs2, 0,
+                                    ptr(nw), float(eps), ptr(h), _lib.stream_of(A))
+    if rc == _lib.QZ_ERR_SHAPE:
+        return None
+    check(rc, "gemv_4bit_pair_silu")
+    return h
+
+
 def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> list:
     """Several batch-1 4-bit GEMVs that share the input vector A, in ONE launch
     (qz_gemv_4bit_grouped).  items: sequence of

@@ -825,11 +825,16 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, bool NRM = false>
-__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block) {
+          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false>
+__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
+                                          const GemvParams *pair = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
   static_assert(!NRM || (NW == 4 && FS && !XL && MODE == kModeTab && (DT == QZ_DT_F16 || DT == QZ_DT_BF16)),
                 "fused pre-norm: 4 waves, full steps, 16-bit activations");
+  // PAIR (LlamaMLP's gate/up): waves 0-1 take R-row groups of pair[0] (gate_proj), waves 2-3 the
+  // same rows of pair[1] (up_proj); the epilogue stores act_fn(gate) * up (k_silu_mul's
+  // arithmetic) for those rows into pair[0].y, the input of down_proj
+  static_assert(!PAIR || (NW == 4 && WK == 1 && MODE == kModeTab && DT != QZ_DT_F32), "pair: 4 waves, WK = 1");
   // WT ("wide table"): 256 B per byte value -- 64 copies of a 4-B entry, or 32 copies of an
   // 8-B exact entry, 64 KiB -- so the lookup address is one v_perm and every copy is bank-private
   constexpr int kPieces = WT ? 16 : kTabCopies / 4;
@@ -845,7 +850,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   constexpr bool kWide = CL || kBF || kF32;
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
-  __shared__ float s_code2[DQ ? 256 : 1];
+  __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
   __shared__ float s_part[NW][R];
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? (WT ? 2 : 1) * kTabDwords : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
@@ -856,7 +861,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int wk = wave % WK;
   const int rg = wave / WK;
-  const int row0 = (block * RG + rg) * R;
+  const int row0 = PAIR ? (block * 2 + (wave & 1)) * R : (block * RG + rg) * R;
+  const int cb = PAIR ? (wave >> 1) : 0;   // this wave's code2 table
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
 
@@ -865,9 +871,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // prologue's global loads (which queue behind the CU's HBM requests)
   constexpr bool kNoPro = (ABL & 32768) != 0;
   // 1. the double-quant code table load goes out first (it gates the barrier)
-  float c2 = 0.0f, offset = 0.0f;
+  float c2 = 0.0f, c2b = 0.0f, offset = 0.0f;
   if constexpr (DQ && !kNoPro) {
-    if (NW * 64 == 256 || threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x & 255];
+    if constexpr (PAIR) {
+      c2 = keep_sp(pair[0].sc.code2)[threadIdx.x];
+      c2b = keep_sp(pair[1].sc.code2)[threadIdx.x];
+    } else if (NW * 64 == 256 || threadIdx.x < 256) {
+      c2 = p.sc.code2[threadIdx.x & 255];
+    }
     offset = *p.sc.offset;
   } else if constexpr (DQ) {
     c2 = (float)(threadIdx.x & 255) * (1.0f / 256.0f);
@@ -930,7 +941,8 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const bool have = s < nsteps;
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
-    if (NW * 64 == 256 || threadIdx.x < 256) s_code2[threadIdx.x & 255] = c2;
+    if (NW * 64 == 256 || threadIdx.x < 256) s_code2[0][threadIdx.x & 255] = c2;
+    if constexpr (PAIR) s_code2[PAIR ? 1 : 0][threadIdx.x] = c2b;
   }
   __shared__ float s_nss[NRM ? 4 : 1];
   if constexpr (NRM) {  // sum of squares: per thread in chunk order, per wave by the xor butterfly
@@ -1039,7 +1051,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float am;
-      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
+      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cb][c.q[r]], c.a[r]), offset);
       else am = c.a[r];
       am = c.on ? am : 0.0f;
       if constexpr (kScaled) am *= usc;  // exact: a power of two (the lane's x pre-scale)
@@ -1086,6 +1098,32 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     return;
   }
   QZ_STAMP(3);
+  if constexpr (PAIR) {  // gate (waves 0-1) and up (waves 2-3) of the same rows meet in LDS
+    float v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        float o = v[r] * out_scale;
+        if (p.bias) o += load_f32<DT>(p.bias, min(row0 + r, p.M - 1));
+        s_part[wave][r] = o;
+      }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < 2 * R) {
+      const int g2 = threadIdx.x / R, r = threadIdx.x % R;
+      const int row = (block * 2 + g2) * R + r;
+      if (row < p.M) {
+        // h = act_fn(gate) * up on the projections as torch stores them; k_silu_mul's
+        // x / (1 + exp(-x)) rounded, then the product rounded by the store
+        const float gv = round_store<DT>(s_part[g2][r]), uv = round_store<DT>(s_part[2 + g2][r]);
+        const float a = round_store<DT>(__fdiv_rn(gv, __fadd_rn(1.0f, expf(-gv))));
+        store_f32<DT>(keep_sp(pair[0].y), row, __fmul_rn(a, uv));
+      }
+    }
+    return;
+  }
   if constexpr (WK == 1) {  // the wave owns whole rows: lane 63 reduces and stores them
     float v[R];
 #pragma unroll
@@ -1286,6 +1324,14 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
   gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, false, NRM>(seg, b - start);
+}
+
+// LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
+template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM>
+__global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+  const GemvParams seg = g.seg[wave >> 1];
+  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -1688,4 +1734,67 @@ extern "C" int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *seg
                                             const void *norm_weight, float eps, void *stream) {
   if (!norm_weight || !x) return QZ_ERR_ARG;
   return gemv_grouped_impl(nseg, segs, K, x, dtype, quant_type, blocksize, blocksize2, lut, norm_weight, eps, stream);
+}
+
+// LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (modeling_llama.py:175, hidden_act "silu") in one
+// launch: segs[0] = gate, segs[1] = up (equal M; their y are not written), h = the [M] product
+extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
+                                      int blocksize, int blocksize2, const float *lut, const void *norm_weight,
+                                      float eps, void *h, void *stream) {
+  if (!segs || !h || !x) return QZ_ERR_ARG;
+  if (segs[0].M != segs[1].M) return QZ_ERR_SHAPE;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_SHAPE;
+  GemvGroup g;
+  g.nseg = 2;
+  const bool cl = exact_codes(quant_type, lut) && dtype == QZ_DT_F16;
+  const bool dq = segs[0].qabsmax != nullptr;
+  for (int i = 0; i < 2; ++i) {
+    const qz_gemv_segment &q = segs[i];
+    bool v;
+    const int st = make_params(q.M, K, x, dtype, q.B, quant_type, blocksize, q.absmax, q.qabsmax, q.absmax2, q.code2,
+                               q.offset, blocksize2, q.block_base, lut, q.bias, h, &g.seg[i], &v);
+    if (st != QZ_OK) return st;
+    if ((q.qabsmax != nullptr) != dq || !v || !full_steps(K, blocksize, blocksize2, dq, q.block_base))
+      return QZ_ERR_SHAPE;
+    set_tables(quant_type & ~QZ_EXACT_CODES, lut, cl, dtype, &g.seg[i]);
+    g.seg[i].nw = norm_weight;
+    g.seg[i].eps = eps;
+  }
+  const int M = segs[0].M;
+  if (M == 0) return QZ_OK;
+  if (norm_weight && (K % 8 != 0 || K > 16384 || ((uintptr_t)x | (uintptr_t)norm_weight) % 16 != 0))
+    return QZ_ERR_SHAPE;
+  // the geometry qz_gemv_4bit_grouped takes for the pair's 2M rows (same per-row summation order,
+  // so the same bits); the epilogue needs whole rows per wave: splits along K (WK > 1, e.g. the
+  // K = 8192 layers) and single-row waves are left to the two-launch form
+  int R, WK;
+  choose_geometry(2 * M, K, dtype, &R, &WK);
+  if (WK != 1 || R < 2) return QZ_ERR_SHAPE;
+  const int blocks = (M + 2 * R - 1) / (2 * R);
+  if (norm_weight && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
+  for (int i = 2; i < kMaxSeg; ++i) g.start[i] = 0;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = norm_weight ? (size_t)K * 2 : 0;
+#define QZ_PS(DQ_, DT_, RR, CL_, NRM_) \
+  hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_>), dim3(blocks), dim3(256), lds, s, g)
+#define QZ_PS_R(DQ_, DT_, CL_, NRM_)           \
+  do {                                          \
+    if (R == 4) QZ_PS(DQ_, DT_, 4, CL_, NRM_);  \
+    else QZ_PS(DQ_, DT_, 2, CL_, NRM_);         \
+  } while (0)
+#define QZ_PS_N(DQ_, DT_, CL_)                                                      \
+  do {                                                                              \
+    if (norm_weight) QZ_PS_R(DQ_, DT_, CL_, true); else QZ_PS_R(DQ_, DT_, CL_, false); \
+  } while (0)
+  if (dtype == QZ_DT_F16) {
+    if (dq) { if (cl) QZ_PS_N(true, QZ_DT_F16, true); else QZ_PS_N(true, QZ_DT_F16, false); }
+    else { if (cl) QZ_PS_N(false, QZ_DT_F16, true); else QZ_PS_N(false, QZ_DT_F16, false); }
+  } else {
+    if (dq) QZ_PS_N(true, QZ_DT_BF16, false); else QZ_PS_N(false, QZ_DT_BF16, false);
+  }
+#undef QZ_PS_N
+#undef QZ_PS_R
+#undef QZ_PS
+  QZ_LAUNCH_CHECK();
+  return QZ_OK;
 }

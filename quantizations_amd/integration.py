@@ -230,13 +230,21 @@ def _fused_rope(orig):
     return apply_rotary_pos_emb
 
 
-def _fused_mlp_forward(mod: nn.Module):
+def _fused_mlp_forward(mod: nn.Module, pair: bool = True):
     from .layer_ops import silu_mul, silu_mul_supported
 
+    from .modules import linear4bit_silu_pair
+
     def forward(x: torch.Tensor, _qz_residual=None) -> torch.Tensor:
-        g = mod.gate_proj(x)  # same call order as LlamaMLP.forward (a DecodeGroup launches gate+up here)
-        u = mod.up_proj(x)
-        h = silu_mul(g, u) if silu_mul_supported(g, u) else mod.act_fn(g) * u
+        h = None
+        grp = mod.gate_proj.__dict__.get("_qz_group")
+        if pair and grp is not None and len(grp.members) == 2 and grp.members[0] is mod.gate_proj and \
+                grp.members[1] is mod.up_proj:
+            h = linear4bit_silu_pair(grp, x)   # gate, up and their product: one launch
+        if h is None:
+            g = mod.gate_proj(x)  # same call order as LlamaMLP.forward (a DecodeGroup launches gate+up here)
+            u = mod.up_proj(x)
+            h = silu_mul(g, u) if silu_mul_supported(g, u) else mod.act_fn(g) * u
         return _project(mod.down_proj, h, _qz_residual)
     return forward
 
@@ -343,7 +351,8 @@ def _fused_decoder_forward(mod: nn.Module):
 
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
-                   decoder: bool = False, attention: bool = True, residual: bool = True) -> int:
+                   decoder: bool = False, attention: bool = True, residual: bool = True,
+                   mlp_pair: bool = True) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -356,7 +365,9 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     `attention` routes a decode step's rotary + StaticCache update + sdpa attention of
     each Llama/Mistral/Qwen2 attention module through layer_ops.decode_attention (counted
     once per module).  `residual` (with `attention` and `mlp`) moves each decoder layer's two
-    residual adds into the o_proj / down_proj GEMV epilogues (counted once per layer)."""
+    residual adds into the o_proj / down_proj GEMV epilogues (counted once per layer).
+    `mlp_pair` lets a fused MLP compute gate/up and act_fn(gate) * up in one launch
+    (modules.linear4bit_silu_pair) where its projections form a decode group."""
     import sys
 
     n = 0
@@ -375,7 +386,7 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
         elif mlp and name in MLP_CLASSES and "forward" not in m.__dict__ and \
                 "silu" in type(getattr(m, "act_fn", None)).__name__.lower() and \
                 all(hasattr(m, p) for p in ("gate_proj", "up_proj", "down_proj")):
-            m.__dict__["forward"] = _fused_mlp_forward(m)
+            m.__dict__["forward"] = _fused_mlp_forward(m, pair=mlp_pair)
             m.__dict__["_qz_fused_mlp"] = True
             n += 1
         elif (rope or attention) and name in ATTENTION_CLASSES:

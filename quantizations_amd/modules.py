@@ -15,7 +15,7 @@ import torch.nn as nn
 
 from . import _lib
 from .core import (MT_MAX_TOKENS, Params4bit, QuantState, dequantize_4bit, exact_codes_for, gemm_4bit,
-                   gemm_4bit_grouped, gemv_4bit, gemv_4bit_grouped, grouped_tokens_ok)
+                   gemm_4bit_grouped, gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, grouped_tokens_ok)
 
 
 def matmul_4bit(A: torch.Tensor, B: torch.Tensor, quant_state: QuantState, out: torch.Tensor = None, bias=None,
@@ -97,6 +97,31 @@ def _linear4bit_group_compute(group: DecodeGroup, x: torch.Tensor):
         outs = [matmul_4bit(xin, w, bias=b, quant_state=st, exact_codes=exact_codes_for(m0.compute_dtype))
                 for w, st, b in items]
     return [o if o.dtype == inp_dtype else o.to(inp_dtype) for o in outs]
+
+
+def linear4bit_silu_pair(group: DecodeGroup, x: torch.Tensor):
+    """act_fn(gate_proj(x)) * up_proj(x) for a decode group of exactly (gate_proj, up_proj) and a
+    single token, in one launch (core.gemv_4bit_pair_silu; an RMSNorm absorbed by fuse_prenorm
+    is applied inside too).  None when that launch does not take the case: the caller then calls
+    the members (the grouped launch) and multiplies."""
+    if group._compute is not _linear4bit_group_compute or len(group.members) != 2:
+        return None
+    if not (x.is_cuda and x.numel() == x.shape[-1] and x.dtype in (torch.float16, torch.bfloat16)):
+        return None
+    for m in group.members:
+        if m.weight.quant_state is None:
+            return None
+        if not m.compute_type_is_set:
+            m.set_compute_type(x)
+            m.compute_type_is_set = True
+    m0, m1 = group.members
+    if m0._input(x) is not x or m1._input(x) is not x or \
+            exact_codes_for(m0.compute_dtype) != exact_codes_for(m1.compute_dtype):
+        return None
+    norm = group.prenorm
+    items = [(m.weight, m.weight.quant_state, None if m.bias is None else m.bias.to(x.dtype)) for m in group.members]
+    return gemv_4bit_pair_silu(x, items, exact_codes=exact_codes_for(m0.compute_dtype),
+                               norm=None if norm is None else norm[:2])
 
 
 class Linear4bit(nn.Linear):

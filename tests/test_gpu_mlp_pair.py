@@ -1,0 +1,116 @@
+"""GPU: LlamaMLP's gate/up projections and act_fn(gate) * up in ONE launch
+(qz_gemv_4bit_pair_silu, core.gemv_4bit_pair_silu, modules.linear4bit_silu_pair).
+
+The bar is bit-identity with the grouped launch followed by the separate product -- and with
+torch's own F.silu(g) * u on those outputs -- for fp16 (exact and fp16-rounded NF4 codes) and
+bf16, FP4 without double quant, with and without a bias and with the absorbed RMSNorm; and a
+Llama model whose MLPs run the pair launch decodes bit-identical logits to transformers' MLP.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda")
+
+
+def _items(M, K, dtype, seed, quant="nf4", dq=True, bias=False):
+    from quantizations_amd.core import quantize_4bit
+
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    items = []
+    for _ in range(2):
+        W = (torch.randn(M, K, device=DEV, generator=g) * 0.02).to(dtype)
+        packed, st = quantize_4bit(W, quant_type=quant, compress_statistics=dq)
+        b = (torch.randn(M, device=DEV, generator=g) * 0.1).to(dtype) if bias else None
+        items.append((packed, st, b))
+    return items
+
+
+@pytest.mark.parametrize("dtype,exact", [(torch.float16, True), (torch.float16, None), (torch.bfloat16, None)])
+@pytest.mark.parametrize("M,K,norm,bias", [(14336, 4096, True, False), (14336, 4096, False, False),
+                                           (3000, 2048, True, True), (4096, 6144, False, True)])
+def test_pair_silu_bit_identical_to_grouped_plus_product(dtype, exact, M, K, norm, bias):
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
+    from quantizations_amd.layer_ops import silu_mul
+
+    items = _items(M, K, dtype, seed=M + K, bias=bias)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).to(dtype)
+    nw = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(dtype) if norm else None
+    nrm = (nw, 1e-5) if norm else None
+    gate, up = gemv_4bit_grouped(x, items, exact_codes=exact, norm=nrm)
+    h = gemv_4bit_pair_silu(x, items, exact_codes=exact, norm=nrm)
+    torch.cuda.synchronize()
+    assert h is not None and h.shape == gate.shape and h.dtype == dtype
+    assert torch.equal(h, silu_mul(gate, up))
+    assert torch.equal(h, F.silu(gate) * up)
+
+
+def test_pair_silu_fp4_without_double_quant():
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
+
+    items = _items(4096, 4096, torch.float16, seed=9, quant="fp4", dq=False)
+    x = torch.randn(1, 1, 4096, device=DEV).half()
+    gate, up = gemv_4bit_grouped(x, items)
+    assert torch.equal(gemv_4bit_pair_silu(x, items), F.silu(gate) * up)
+
+
+def test_pair_silu_declines_what_it_cannot_take():
+    """Geometries that split rows over waves (K = 8192; small pairs), odd K, fp32 x, unequal
+    shapes: None, nothing launched (the grouped launch + product then run)."""
+    from quantizations_amd.core import gemv_4bit_pair_silu
+
+    items = _items(4096, 8192, torch.float16, seed=1)
+    assert gemv_4bit_pair_silu(torch.randn(1, 1, 8192, device=DEV).half(), items) is None
+    items = _items(1000, 6144, torch.float16, seed=7)
+    assert gemv_4bit_pair_silu(torch.randn(1, 1, 6144, device=DEV).half(), items) is None
+    items = _items(512, 1000, torch.float16, seed=2)
+    assert gemv_4bit_pair_silu(torch.randn(1, 1, 1000, device=DEV).half(), items) is None
+    items = _items(512, 2048, torch.float32, seed=3)
+    assert gemv_4bit_pair_silu(torch.randn(1, 1, 2048, device=DEV), items) is None
+    a = _items(512, 2048, torch.float16, seed=4)
+    b = _items(256, 2048, torch.float16, seed=5)
+    assert gemv_4bit_pair_silu(torch.randn(1, 1, 2048, device=DEV).half(), [a[0], b[0]]) is None
+
+
+def test_llama_mlp_pair_logits_bit_identical_to_transformers_mlp():
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from transformers.cache_utils import StaticCache
+
+    from quantizations_amd.integration import (fuse_layer_ops, fuse_prenorm, fuse_projection_groups,
+                                               replace_with_bnb_linear, unfuse_layer_ops)
+
+    cfg = LlamaConfig(hidden_size=2048, intermediate_size=4096, num_hidden_layers=2, num_attention_heads=16,
+                      num_key_value_heads=4, vocab_size=512)
+    torch.manual_seed(8)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, quant_type="nf4", compute_dtype=torch.float32)
+    fuse_projection_groups(model)
+    ids = torch.randint(0, 512, (1, 7), device=DEV, generator=torch.Generator(device="cuda").manual_seed(6))
+
+    def decode():
+        cache = StaticCache(config=cfg, max_cache_len=24)
+        out = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(7, device=DEV))
+        logits = [out.logits[:, -1].clone()]
+        tok = out.logits[:, -1:].argmax(-1)
+        for i in range(5):
+            pos = torch.tensor([7 + i], device=DEV)
+            lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos.view(1, 1)).logits
+            logits.append(lo[:, -1].clone())
+            tok = lo[:, -1:].argmax(-1)
+        return logits
+
+    try:
+        with torch.no_grad():
+            fuse_layer_ops(model, mlp=False)     # transformers' LlamaMLP: act_fn(gate) * up in torch
+            fuse_prenorm(model)
+            ref = decode()
+            unfuse_layer_ops(model)
+            fuse_layer_ops(model)                # the pair launch (+ residual epilogue)
+            fuse_prenorm(model)
+            got = decode()
+            assert all(torch.equal(a, b) for a, b in zip(got, ref))
+    finally:
+        unfuse_layer_ops(model)

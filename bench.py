@@ -454,12 +454,13 @@ assert gemv_alg_bytes([(4096, 4096)]) == GEMV_BYTES_4096
 
 
 @torch.inference_mode()
-def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True):
+def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, pair: bool = True):
     """The decode step's longest Linear4bit launch: the grouped gate/up GEMV of a
     Llama-3-8B layer (2 x 14336x4096 NF4+DQ in ONE launch; with `prenorm`, the
-    post-attention RMSNorm inside it, as the bench decode runs it), rotating weights
-    (8 sets = 485 MB > the 256 MiB Infinity Cache), same timing method."""
-    from quantizations_amd.core import gemv_4bit_grouped, quantize_4bit
+    post-attention RMSNorm inside it; with `pair`, act_fn(gate) * up in its epilogue --
+    as the bench decode runs it), rotating weights (8 sets = 485 MB > the 256 MiB
+    Infinity Cache), same timing method."""
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
 
     dev = torch.device("cuda")
     torch.manual_seed(8)
@@ -478,16 +479,23 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True):
     sets = [[(p, q, b, 0, o) for (p, q, b), o in zip(items, outs)] for items in sets]
     from quantizations_amd.core import exact_codes_for
 
-    def timed(exact, norm):
+    def timed(exact, norm, pr=pair):
         nm = (nw, 1e-5) if norm else None
+
+        def launch(i):
+            if pr:
+                assert gemv_4bit_pair_silu(x, [t[:3] for t in sets[i % copies]], exact_codes=exact,
+                                           norm=nm) is not None
+            else:
+                gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact, norm=nm)
         for i in range(2 * copies):
-            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact, norm=nm)
+            launch(i)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(100_000_000)
         e0.record()
         for i in range(iters):
-            gemv_4bit_grouped(x, sets[i % copies], exact_codes=exact, norm=nm)
+            launch(i)
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / iters
@@ -495,15 +503,17 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True):
     prod = exact_codes_for(torch.float32)      # the bench model's Linear4bit (compute_dtype fp32)
     us = timed(prod, prenorm)
     other_us = timed(not prod, prenorm)
-    plain_us = timed(prod, False) if prenorm else us
-    nbytes = gemv_alg_bytes([(14336, 4096)] * 2) + (4096 * 2 if prenorm else 0)   # + the norm weight
-    return {"kernel": "k_gemv_4bit_grouped gate/up 2 x 14336x4096 NF4+DQ (one launch per layer)"
+    plain_us = timed(prod, False, False) if (prenorm or pair) else us
+    # + the norm weight; the pair writes one [14336] product instead of the two projections
+    nbytes = gemv_alg_bytes([(14336, 4096)] * 2) + (4096 * 2 if prenorm else 0) - (14336 * 2 if pair else 0)
+    return {"kernel": ("k_gemv_4bit_pair gate/up + act_fn(gate) * up" if pair else "k_gemv_4bit_grouped gate/up")
+                      + " 2 x 14336x4096 NF4+DQ (one launch per layer)"
                       + (", post-attention RMSNorm in its prologue" if prenorm else ""),
             "codes": "exact (fp32 as hi+lo fp16)" if prod else "fp16",
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-            "other_codes_launch_us": round(other_us, 3), "without_norm_launch_us": round(plain_us, 3),
+            "other_codes_launch_us": round(other_us, 3), "plain_grouped_launch_us": round(plain_us, 3),
             "traffic": _pmc_traffic("r3_gateup_pmc.json"),
             "profile": "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the "
                        "launch without the norm)"}
@@ -1055,7 +1065,8 @@ def main():
                 "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline(
                     prenorm=bool(not args.no_prenorm and not sharded and not args.no_fuse
-                                 and layer_ops in ("all", "norm")))}
+                                 and layer_ops in ("all", "norm")),
+                    pair=bool(not args.no_mlp_pair and not args.no_fuse and layer_ops in ("all", "all+decoder", "mlp")))}
         from quantizations_amd import _lib, core
         ink = gemv_in_kernel(bool(core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32), torch.float16)
                                   & _lib.EXACT_CODES))

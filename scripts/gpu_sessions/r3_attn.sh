@@ -12,4 +12,4 @@ step() {  # name timeout cmd...
   [ $rc -eq 0 ] || exit $rc
 }
 step r3at_tests 400 python -u -m pytest tests/test_gpu_decode_attention.py tests/test_gpu_layer_ops.py tests/test_gpu_prenorm.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
-step r3at_bench 400 python bench.py --no-prefill --no-cpu
+step r3at_bench 400 python bench.py --no-prefill --no-cpu --no-roofline --no-extra-codes

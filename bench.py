@@ -115,6 +115,23 @@ def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: in
     return dt, torch.cat(toks, dim=1)
 
 
+TWO_STAGE_ARGMAX = True   # --torch-argmax: the decode step's greedy pick as one torch.argmax (A/B)
+
+
+def greedy_token(logits: torch.Tensor) -> torch.Tensor:
+    """argmax over the last dim ([B, 1, V] -> [B, 1]), the first maximal index as torch.argmax
+    returns it, in two parallel stages when V splits into 256-wide rows: a row max with its
+    first index, then the first row holding the global max.  torch's one-pass argmax reduces the
+    128256 Llama-3 logits with a handful of workgroups (43.7 us of a 2 ms decode step,
+    profiles/r3_decode_anatomy_fused.txt); the two stages spread it over 501."""
+    V = logits.shape[-1]
+    if V % 256 or V < 4096:
+        return logits.argmax(-1)
+    m, i = logits.reshape(*logits.shape[:-1], V // 256, 256).max(-1)   # [B, 1, V/256]
+    r = m.argmax(-1, keepdim=True)                                       # first row with the max
+    return (i.gather(-1, r) + r * 256).squeeze(-1)
+
+
 @torch.inference_mode()
 def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, world: int, batch: int = 1,
                        graph: bool = True, device: str = "cuda"):
@@ -142,7 +159,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
     def step():
         lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos_ids,
                    use_cache=True).logits
-        nxt = lo[:, -1:].argmax(-1)
+        nxt = greedy_token(lo[:, -1:]) if TWO_STAGE_ARGMAX else lo[:, -1:].argmax(-1)
         hist.index_copy_(1, pos, nxt.view(batch, 1))
         tok.copy_(nxt)
         pos.add_(1)
@@ -887,6 +904,9 @@ def main():
     ap.add_argument("--no-attention", action="store_true",
                     help="keep transformers' rotary + StaticCache update + sdpa (14 launches per layer) instead of "
                          "the one-launch layer_ops.decode_attention")
+    ap.add_argument("--torch-argmax", action="store_true",
+                    help="the decode step's greedy pick as torch's one-pass argmax (default: greedy_token's two "
+                         "stages, the same index)")
     ap.add_argument("--no-mlp-pair", action="store_true",
                     help="gate/up as the grouped launch + a separate SiLU-product launch (default: one launch)")
     ap.add_argument("--no-residual", action="store_true",
@@ -976,6 +996,8 @@ def main():
     layer_ops = "none" if args.no_layer_ops else args.layer_ops
 
     compute_dtype = torch.float32 if args.compute_dtype == "fp32" else torch.float16
+    global TWO_STAGE_ARGMAX
+    TWO_STAGE_ARGMAX = not args.torch_argmax
 
     def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int, cdt: torch.dtype = compute_dtype):
         t_build = time.perf_counter()
@@ -1121,6 +1143,7 @@ def main():
                                                         and layer_ops in ("all", "all+decoder", "mlp"))
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
+        line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"
         if exchange is not None:
             line["config"]["exchange"] = exchange
         if extra_codes is not None:

@@ -151,6 +151,13 @@ __global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, co
 // probabilities to the storage dtype before P V; this kernel does not), output rounded once.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAttnChunk = 128;  // key positions per workgroup
+// QZ_ATTN_ABL (measurement builds only, scripts/dev/attn_ablation.py; 0 in the product): drop one
+// phase to price it -- 1 the arrival atomic, 2 the cache row loads, 4 P V, 8 the scores,
+// 16 the softmax exponentials, 32 everything after the loads
+#ifndef QZ_ATTN_ABL
+#define QZ_ATTN_ABL 0
+#endif
+constexpr int kAttnAbl = QZ_ATTN_ABL;
 constexpr int kAttnMaxG = 8;     // query heads per kv head
 
 struct DecodeAttnArgs {
@@ -185,109 +192,152 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
   static_assert(ES == 2, "16-bit activations and caches");
   constexpr int H2 = D / 2;  // rotary half; also the share of a row one thread dots
+  constexpr int NW = H2 / 2; // 32-bit words of half a row
   __shared__ float s_q[kAttnMaxG][D];                  // rotated q (storage-rounded values)
-  __shared__ float s_sc[2][kAttnMaxG][kAttnChunk];     // half-row partial scores; [0]: probabilities
+  __shared__ float s_sc[2][kAttnMaxG][kAttnChunk];     // half-row partial scores
+  __shared__ __attribute__((aligned(16))) float s_p[kAttnMaxG][kAttnChunk];  // probabilities (0: masked / past L)
   __shared__ uint32_t s_v[kAttnChunk][H2];             // raw v rows (zero where masked)
   __shared__ uint32_t s_kn[H2], s_vn[H2];              // the new (rotated) k and v, raw
   __shared__ unsigned char s_ok[kAttnChunk];
-  __shared__ float s_m[kAttnMaxG], s_l[kAttnMaxG];
+  __shared__ float s_l[kAttnMaxG], s_m[kAttnMaxG];
 
   const int t = threadIdx.x, split = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int G = a.G, L = a.L;
   const int j0 = split * kAttnChunk;
-  const long long p = *a.pos;
-  const bool mine = p >= j0 && p < j0 + kAttnChunk && p < L;  // this chunk holds the new token
   const long long crow = ((long long)b * a.Hkv + h) * L;     // first cache row of (b, h)
+  const int pos_i = t & (kAttnChunk - 1), half = t >> 7;     // this thread's key position / row half
+  const long long j = j0 + pos_i;
+  const bool in_l = j < L;
+
+  // 0. Every global load goes out before anything waits (latency, not bandwidth, bounds a
+  //    decode step's attention): p, this thread's q / cos / sin operands, the new k and v, then
+  //    the mask byte and the half rows of k and v at position j -- whatever the mask says
+  //    (a masked row is dropped after it arrives) -- so the cache reads overlap the rotary.
+  const long long p = *a.pos;
+  const char *cb = reinterpret_cast<const char *>(a.cos) + (long long)b * a.cs * ES;
+  const char *sb = reinterpret_cast<const char *>(a.sin) + (long long)b * a.cs * ES;
+  const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)h * G * D) * ES;
+  const int gq = t / H2, dq = t - gq * H2;                   // the (head, pair) this thread rotates
+  const bool do_q = t < G * H2;                              // G * H2 <= 8 * 64 = 512: two rounds at most
+  const int gq2 = (t + 256) / H2, dq2 = t + 256 - gq2 * H2;
+  const bool do_q2 = t + 256 < G * H2;
+  float x1 = 0.f, x2 = 0.f, y1 = 0.f, y2 = 0.f, c1 = 0.f, c2 = 0.f, s1 = 0.f, s2 = 0.f;
+  const int dr = t & (H2 - 1);                               // == dq (and == dq2; == t below H2)
+  c1 = load_f32<DT>(cb, dr); c2 = load_f32<DT>(cb, dr + H2);
+  s1 = load_f32<DT>(sb, dr); s2 = load_f32<DT>(sb, dr + H2);
+  if (do_q) { x1 = load_f32<DT>(qb + (long long)gq * D * ES, dq); x2 = load_f32<DT>(qb + (long long)gq * D * ES, dq + H2); }
+  if (do_q2) { y1 = load_f32<DT>(qb + (long long)gq2 * D * ES, dq2); y2 = load_f32<DT>(qb + (long long)gq2 * D * ES, dq2 + H2); }
+  float k1 = 0.f, k2 = 0.f;
+  uint32_t vnew = 0u;
+  if (t < H2) {
+    const char *kb = reinterpret_cast<const char *>(a.k) + ((long long)b * a.ks + (long long)h * D) * ES;
+    const char *vb = reinterpret_cast<const char *>(a.v) + ((long long)b * a.vs + (long long)h * D) * ES;
+    k1 = load_f32<DT>(kb, t); k2 = load_f32<DT>(kb, t + H2);
+    vnew = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
+  }
+  const unsigned char mk = in_l ? a.mask[(long long)b * a.mb + j * a.mj] : (unsigned char)0;
+  u32x4 kr[NW / 4], vr[NW / 4];
+  if (in_l && (kAttnAbl & 2) == 0) {
+    const u32x4 *kp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.kc) + ((crow + j) * D + half * H2) * ES);
+    const u32x4 *vp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.vc) + ((crow + j) * D + half * H2) * ES);
+#pragma unroll
+    for (int i = 0; i < NW / 4; ++i) kr[i] = kp[i];
+#pragma unroll
+    for (int i = 0; i < NW / 4; ++i) vr[i] = vp[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NW / 4; ++i) kr[i] = vr[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __builtin_amdgcn_sched_barrier(0);
 
   // 1. rotary of the G query heads (and, in the chunk holding p, of the new key), k_rope_qk's
   //    arithmetic: q*cos + cat(-x2, x1)*sin with every torch op rounded to the storage dtype
-  const char *cb = reinterpret_cast<const char *>(a.cos) + (long long)b * a.cs * ES;
-  const char *sb = reinterpret_cast<const char *>(a.sin) + (long long)b * a.cs * ES;
-  auto rope = [&](const char *x, int d, float &lo, float &hi) {
-    const float x1 = load_f32<DT>(x, d), x2 = load_f32<DT>(x, d + H2);
-    const float c1 = load_f32<DT>(cb, d), c2 = load_f32<DT>(cb, d + H2);
-    const float s1 = load_f32<DT>(sb, d), s2 = load_f32<DT>(sb, d + H2);
-    lo = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(x1, c1)), round_dt<DT>(__fmul_rn(-x2, s1)))));
-    hi = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(x2, c2)), round_dt<DT>(__fmul_rn(x1, s2)))));
+  auto rope = [&](float u1, float u2, float &lo, float &hi) {
+    lo = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(u1, c1)), round_dt<DT>(__fmul_rn(-u2, s1)))));
+    hi = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(u2, c2)), round_dt<DT>(__fmul_rn(u1, s2)))));
   };
-  const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)h * G * D) * ES;
-  for (int i = t; i < G * H2; i += 256) {
-    const int g = i / H2, d = i - g * H2;
+  if (do_q) {
     float lo, hi;
-    rope(qb + (long long)g * D * ES, d, lo, hi);
-    s_q[g][d] = lo;
-    s_q[g][d + H2] = hi;
+    rope(x1, x2, lo, hi);
+    s_q[gq][dq] = lo;
+    s_q[gq][dq + H2] = hi;
   }
-  if (mine && t < H2) {
-    const char *kb = reinterpret_cast<const char *>(a.k) + ((long long)b * a.ks + (long long)h * D) * ES;
-    const char *vb = reinterpret_cast<const char *>(a.v) + ((long long)b * a.vs + (long long)h * D) * ES;
+  if (do_q2) {  // G * H2 > 256 (D = 128, G > 4): dq2 == dq, so this thread's cos / sin apply
     float lo, hi;
-    rope(kb, t, lo, hi);
+    rope(y1, y2, lo, hi);
+    s_q[gq2][dq2] = lo;
+    s_q[gq2][dq2 + H2] = hi;
+  }
+  const bool mine = p >= j0 && p < j0 + kAttnChunk && p < L;  // this chunk holds the new token
+  if (mine && t < H2) {  // t < H2: dr == t
+    float lo, hi;
+    rope(k1, k2, lo, hi);
     char *kd = reinterpret_cast<char *>(a.kc) + (crow + p) * D * ES;
     char *vd = reinterpret_cast<char *>(a.vc) + (crow + p) * D * ES;
     store_f32<DT>(kd, t, lo);
     store_f32<DT>(kd, t + H2, hi);
-    const uint32_t vw = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
-    reinterpret_cast<uint32_t *>(vd)[t] = vw;
-    s_vn[t] = vw;
+    reinterpret_cast<uint32_t *>(vd)[t] = vnew;
+    s_vn[t] = vnew;
     // the rotated k as raw elements: element e in the 16-bit half e % 2 of s_kn[e / 2]
     reinterpret_cast<uint16_t *>(s_kn)[t] = (uint16_t)bits_dt<DT>(lo);
     reinterpret_cast<uint16_t *>(s_kn)[t + H2] = (uint16_t)bits_dt<DT>(hi);
   }
-  if (t < kAttnChunk) {
-    const int j = j0 + t;
-    s_ok[t] = (j < L && a.mask[(long long)b * a.mb + (long long)j * a.mj] != 0) ? 1 : 0;
-  }
   __syncthreads();
+  if constexpr ((kAttnAbl & 32) != 0) {
+    if (t < 2 * H2) { float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) acc += __uint_as_float(kr[i].x ^ vr[i].y);
+      reinterpret_cast<float *>(a.out)[t] = acc + s_q[0][t & (D - 1)]; }
+    return;
+  }
 
   // 2. half-row dot products: thread t scores position t % 128 over dims [H2 * (t / 128), + H2)
-  //    and stages that half of the position's v row in LDS
+  //    and stages that half of the position's v row in LDS (zeros where masked / past L)
   {
-    const int pos = t & (kAttnChunk - 1), half = t >> 7;
-    const long long j = j0 + pos;
-    const bool ok = s_ok[pos] != 0;
-    constexpr int NW = H2 / 2;  // 32-bit words of half a row
+    const bool ok = mk != 0;
     uint32_t kw[NW], vw[NW];
     if (ok && j == p) {
 #pragma unroll
       for (int i = 0; i < NW; ++i) { kw[i] = s_kn[half * NW + i]; vw[i] = s_vn[half * NW + i]; }
-    } else if (ok) {
-      const u32x4 *kr = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.kc) + ((crow + j) * D + half * H2) * ES);
-      const u32x4 *vr = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.vc) + ((crow + j) * D + half * H2) * ES);
-#pragma unroll
-      for (int i = 0; i < NW / 4; ++i) {
-        const u32x4 x = kr[i], y = vr[i];
-        kw[4 * i] = x.x; kw[4 * i + 1] = x.y; kw[4 * i + 2] = x.z; kw[4 * i + 3] = x.w;
-        vw[4 * i] = y.x; vw[4 * i + 1] = y.y; vw[4 * i + 2] = y.z; vw[4 * i + 3] = y.w;
-      }
     } else {
 #pragma unroll
-      for (int i = 0; i < NW; ++i) kw[i] = vw[i] = 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < NW; ++i) s_v[pos][half * NW + i] = vw[i];
-    for (int g = 0; g < G; ++g) {
-      const float *qg = &s_q[g][half * H2];
-      float acc = 0.0f;
-#pragma unroll
-      for (int i = 0; i < NW; ++i) {
-        acc = fmaf(from_bits<DT>(kw[i]), qg[2 * i], acc);
-        acc = fmaf(from_bits<DT>(kw[i] >> 16), qg[2 * i + 1], acc);
+      for (int i = 0; i < NW / 4; ++i) {
+        kw[4 * i] = kr[i].x; kw[4 * i + 1] = kr[i].y; kw[4 * i + 2] = kr[i].z; kw[4 * i + 3] = kr[i].w;
+        vw[4 * i] = vr[i].x; vw[4 * i + 1] = vr[i].y; vw[4 * i + 2] = vr[i].z; vw[4 * i + 3] = vr[i].w;
       }
-      s_sc[half][g][pos] = acc;
+      if (!ok) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) kw[i] = vw[i] = 0u;
+      }
+    }
+    if (half == 0) s_ok[pos_i] = ok ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) s_v[pos_i][half * NW + i] = vw[i];
+    for (int g = 0; g < ((kAttnAbl & 8) ? 0 : G); ++g) {
+      const float *qg = &s_q[g][half * H2];
+      float acc0 = 0.0f, acc1 = 0.0f;  // two chains: even / odd words
+#pragma unroll
+      for (int i = 0; i < NW; i += 2) {
+        acc0 = fmaf(from_bits<DT>(kw[i]), qg[2 * i], acc0);
+        acc0 = fmaf(from_bits<DT>(kw[i] >> 16), qg[2 * i + 1], acc0);
+        acc1 = fmaf(from_bits<DT>(kw[i + 1]), qg[2 * i + 2], acc1);
+        acc1 = fmaf(from_bits<DT>(kw[i + 1] >> 16), qg[2 * i + 3], acc1);
+      }
+      s_sc[half][g][pos_i] = __fadd_rn(acc0, acc1);
     }
   }
   __syncthreads();
 
-  // 3. softmax statistics: 32 threads per query head, 4 positions each
+  // 3. softmax statistics: 32 threads per query head, 4 positions each; probabilities to s_p
+  //    (their own buffer: no barrier between the score reads and the probability writes)
   {
     const int g = t >> 5, i = t & 31;
     const int gg = g < G ? g : 0;
     float s[4], m = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int pos = 4 * i + r;
-      s[r] = s_ok[pos] ? __fmul_rn(__fadd_rn(s_sc[0][gg][pos], s_sc[1][gg][pos]), a.scale) : -INFINITY;
+      const int pi = 4 * i + r;
+      s[r] = s_ok[pi] ? __fmul_rn(__fadd_rn(s_sc[0][gg][pi], s_sc[1][gg][pi]), a.scale) : -INFINITY;
       m = fmaxf(m, s[r]);
     }
 #pragma unroll
@@ -295,31 +345,38 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
     float l = 0.0f, e[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      e[r] = s[r] == -INFINITY ? 0.0f : expf(s[r] - m);
+      e[r] = s[r] == -INFINITY ? 0.0f : ((kAttnAbl & 16) ? s[r] - m : expf(s[r] - m));
       l += e[r];
     }
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, kWave);
-    __syncthreads();  // every read of s_sc[0] above is done before it is overwritten
     if (g < G) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s_sc[0][g][4 * i + r] = e[r];
+      *reinterpret_cast<float4 *>(&s_p[g][4 * i]) = make_float4(e[0], e[1], e[2], e[3]);
       if (i == 0) { s_m[g] = m; s_l[g] = l; }
     }
   }
   __syncthreads();
 
-  // 4. P V: one output pair (2 dims of one query head) per thread and iteration
-  const int n = min(kAttnChunk, L - j0);
+  // 4. P V: one output pair (2 dims of one query head) per thread and round; 8 positions per
+  //    iteration (one 2 x 16-B probability read), two accumulator chains
+  const int n8 = (min(kAttnChunk, L - j0) + 7) & ~7;   // rows past n are zero in s_v and s_p
   for (int o = t; o < G * H2; o += 256) {
     const int g = o / H2, w = o - g * H2;
-    float acc0 = 0.0f, acc1 = 0.0f;
-    for (int pos = 0; pos < n; ++pos) {
-      const float pr = s_sc[0][g][pos];
-      const uint32_t vv = s_v[pos][w];
-      acc0 = fmaf(pr, from_bits<DT>(vv), acc0);
-      acc1 = fmaf(pr, from_bits<DT>(vv >> 16), acc1);
+    float e0 = 0.0f, e1 = 0.0f, d0 = 0.0f, d1 = 0.0f;
+    for (int q0 = 0; q0 < ((kAttnAbl & 4) ? 0 : n8); q0 += 8) {
+      const float4 pa = *reinterpret_cast<const float4 *>(&s_p[g][q0]);
+      const float4 pb = *reinterpret_cast<const float4 *>(&s_p[g][q0 + 4]);
+      const float pr[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        const uint32_t va = s_v[q0 + r][w], vb2 = s_v[q0 + r + 1][w];
+        e0 = fmaf(pr[r], from_bits<DT>(va), e0);
+        e1 = fmaf(pr[r], from_bits<DT>(va >> 16), e1);
+        d0 = fmaf(pr[r + 1], from_bits<DT>(vb2), d0);
+        d1 = fmaf(pr[r + 1], from_bits<DT>(vb2 >> 16), d1);
+      }
     }
+    const float acc0 = __fadd_rn(e0, d0), acc1 = __fadd_rn(e1, d1);
     if (a.nsplit == 1) {
       const float inv_l = s_l[g];
       char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)(h * G + g) * D) * ES;
@@ -335,7 +392,7 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
 
   // 5. the last workgroup to arrive advances the cache position (every workgroup has read p)
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && (kAttnAbl & 1) == 0) {
     const unsigned int total = gridDim.x * gridDim.y * gridDim.z;
     if (atomicAdd(a.arrive, 1u) == total - 1u) {
       *a.pos = p + 1;

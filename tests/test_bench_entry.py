@@ -49,3 +49,18 @@ def test_bench_world_size_mismatch_exits_nonzero():
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert "WORLD_SIZE=1" in p.stderr
+
+
+def test_greedy_token_is_torch_argmax():
+    """The bench's two-stage greedy pick returns torch.argmax's index (the first maximal one),
+    ties included, at the Llama-3 vocabulary and at a width it hands straight to argmax."""
+    import torch
+    sys.path.insert(0, REPO)
+    from bench import greedy_token
+    for seed in range(24):
+        g = torch.Generator().manual_seed(seed)
+        for V in (128256, 1000):
+            x = torch.randn(2, 1, V, generator=g).half()
+            if seed % 2:
+                x = (x * 2).round().clamp(-3, 3)   # thousands of tied maxima
+            assert torch.equal(greedy_token(x), x.argmax(-1))

@@ -143,9 +143,12 @@ __global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, co
 // (cache_utils.py:455-487: keys/values[:, :, p] = k, v and p += 1) and the masked GQA
 // softmax(q k^T * scale) v of sdpa_attention_forward -- in eager torch 14 launches per layer
 // (rope, arange, two int64 adds, two index_copy_, two repeat_kv copies, the bool-mask
-// conversion, attn_fwd).  Grid (nsplit, Hkv, B): a workgroup takes the G = Hq / Hkv query
-// heads of one kv head over kAttnChunk key positions; nsplit > 1 leaves per-chunk partials
-// (max, sum, unnormalised output) that k_decode_attn_combine merges.
+// conversion, attn_fwd).  Grid (nsplit, Hq, B): a workgroup takes ONE query head over
+// kAttnChunk key positions (the G workgroups of a kv head read its cache rows G times, from L2:
+// the per-workgroup serial work -- the scores and P V, measured at 3.2 and 3.3 us of a 10.1 us
+// launch with G = 4 heads per workgroup, profiles/r3_attn_ablation_g4.txt -- is what bounds a
+// decode step's attention, not bandwidth); nsplit > 1 leaves per-chunk partials (max, sum,
+// unnormalised output) that k_decode_attn_combine merges.
 // Numerics: q and k are rotated with k_rope_qk's per-op rounding (the cache receives the
 // bit-identical k), scores and probabilities stay fp32 (SDPA's flash kernel rounds the
 // probabilities to the storage dtype before P V; this kernel does not), output rounded once.
@@ -159,6 +162,7 @@ constexpr int kAttnChunk = 128;  // key positions per workgroup
 #endif
 constexpr int kAttnAbl = QZ_ATTN_ABL;
 constexpr int kAttnMaxG = 8;     // query heads per kv head
+constexpr int kAttnSpecL = 512;  // caches read before their mask arrives (speculatively) up to this length
 
 struct DecodeAttnArgs {
   const void *q, *k, *v;     // projection outputs, row b at b * {qs, ks, vs} elements, head-major
@@ -191,55 +195,55 @@ template <int DT, int D>
 __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
   static_assert(ES == 2, "16-bit activations and caches");
-  constexpr int H2 = D / 2;  // rotary half; also the share of a row one thread dots
-  constexpr int NW = H2 / 2; // 32-bit words of half a row
-  __shared__ float s_q[kAttnMaxG][D];                  // rotated q (storage-rounded values)
-  __shared__ float s_sc[2][kAttnMaxG][kAttnChunk];     // half-row partial scores
-  __shared__ __attribute__((aligned(16))) float s_p[kAttnMaxG][kAttnChunk];  // probabilities (0: masked / past L)
+  constexpr int H2 = D / 2;      // rotary half; also the share of a row one thread dots
+  constexpr int NW = H2 / 2;     // 32-bit words of half a row
+  constexpr int NSUB = kWave / H2;  // P V: lane groups per wave (D = 128: 1, D = 64: 2)
+  __shared__ float s_q[D];                             // rotated q (storage-rounded values)
+  __shared__ float s_sc[2][kAttnChunk];                // half-row partial scores
+  __shared__ float s_p[kAttnChunk];                    // probabilities (0: masked / past L)
   __shared__ uint32_t s_v[kAttnChunk][H2];             // raw v rows (zero where masked)
   __shared__ uint32_t s_kn[H2], s_vn[H2];              // the new (rotated) k and v, raw
   __shared__ unsigned char s_ok[kAttnChunk];
-  __shared__ float s_l[kAttnMaxG], s_m[kAttnMaxG];
+  __shared__ float s_pv[4 * NSUB][D];                  // P V partials of the position slices
+  __shared__ float s_ml[2];                            // max, sum of this chunk
 
-  const int t = threadIdx.x, split = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int t = threadIdx.x, split = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int G = a.G, L = a.L;
+  const int h = hq / G, gq = hq - h * G;                     // kv head, query head within it
   const int j0 = split * kAttnChunk;
   const long long crow = ((long long)b * a.Hkv + h) * L;     // first cache row of (b, h)
   const int pos_i = t & (kAttnChunk - 1), half = t >> 7;     // this thread's key position / row half
   const long long j = j0 + pos_i;
   const bool in_l = j < L;
 
-  // 0. Every global load goes out before anything waits (latency, not bandwidth, bounds a
-  //    decode step's attention): p, this thread's q / cos / sin operands, the new k and v, then
-  //    the mask byte and the half rows of k and v at position j -- whatever the mask says
-  //    (a masked row is dropped after it arrives) -- so the cache reads overlap the rotary.
+  // 0. Every global load goes out before anything waits (a decode step's attention is bound by
+  //    latency, not bandwidth): p, the q / cos / sin / new k and v operands of the rotary
+  //    (threads below H2: one pair each), then the mask byte and the half rows of k and v at
+  //    position j -- whatever the mask says (a masked row is dropped after it arrives) -- for
+  //    caches up to kAttnSpecL positions; a longer cache is read after its mask, so a long
+  //    static cache early in a sequence does not stream its masked rows.
   const long long p = *a.pos;
-  const char *cb = reinterpret_cast<const char *>(a.cos) + (long long)b * a.cs * ES;
-  const char *sb = reinterpret_cast<const char *>(a.sin) + (long long)b * a.cs * ES;
-  const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)h * G * D) * ES;
-  const int gq = t / H2, dq = t - gq * H2;                   // the (head, pair) this thread rotates
-  const bool do_q = t < G * H2;                              // G * H2 <= 8 * 64 = 512: two rounds at most
-  const int gq2 = (t + 256) / H2, dq2 = t + 256 - gq2 * H2;
-  const bool do_q2 = t + 256 < G * H2;
-  float x1 = 0.f, x2 = 0.f, y1 = 0.f, y2 = 0.f, c1 = 0.f, c2 = 0.f, s1 = 0.f, s2 = 0.f;
-  const int dr = t & (H2 - 1);                               // == dq (and == dq2; == t below H2)
-  c1 = load_f32<DT>(cb, dr); c2 = load_f32<DT>(cb, dr + H2);
-  s1 = load_f32<DT>(sb, dr); s2 = load_f32<DT>(sb, dr + H2);
-  if (do_q) { x1 = load_f32<DT>(qb + (long long)gq * D * ES, dq); x2 = load_f32<DT>(qb + (long long)gq * D * ES, dq + H2); }
-  if (do_q2) { y1 = load_f32<DT>(qb + (long long)gq2 * D * ES, dq2); y2 = load_f32<DT>(qb + (long long)gq2 * D * ES, dq2 + H2); }
-  float k1 = 0.f, k2 = 0.f;
+  const bool rt = t < H2;
+  float x1 = 0.f, x2 = 0.f, c1 = 0.f, c2 = 0.f, s1 = 0.f, s2 = 0.f, k1 = 0.f, k2 = 0.f;
   uint32_t vnew = 0u;
-  if (t < H2) {
+  if (rt) {
+    const char *cb = reinterpret_cast<const char *>(a.cos) + (long long)b * a.cs * ES;
+    const char *sb = reinterpret_cast<const char *>(a.sin) + (long long)b * a.cs * ES;
+    const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)hq * D) * ES;
     const char *kb = reinterpret_cast<const char *>(a.k) + ((long long)b * a.ks + (long long)h * D) * ES;
     const char *vb = reinterpret_cast<const char *>(a.v) + ((long long)b * a.vs + (long long)h * D) * ES;
+    x1 = load_f32<DT>(qb, t); x2 = load_f32<DT>(qb, t + H2);
+    c1 = load_f32<DT>(cb, t); c2 = load_f32<DT>(cb, t + H2);
+    s1 = load_f32<DT>(sb, t); s2 = load_f32<DT>(sb, t + H2);
     k1 = load_f32<DT>(kb, t); k2 = load_f32<DT>(kb, t + H2);
     vnew = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
   }
   const unsigned char mk = in_l ? a.mask[(long long)b * a.mb + j * a.mj] : (unsigned char)0;
   u32x4 kr[NW / 4], vr[NW / 4];
-  if (in_l && (kAttnAbl & 2) == 0) {
-    const u32x4 *kp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.kc) + ((crow + j) * D + half * H2) * ES);
-    const u32x4 *vp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.vc) + ((crow + j) * D + half * H2) * ES);
+  const bool spec = L <= kAttnSpecL;
+  const u32x4 *kp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.kc) + ((crow + j) * D + half * H2) * ES);
+  const u32x4 *vp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(a.vc) + ((crow + j) * D + half * H2) * ES);
+  if (in_l && spec && (kAttnAbl & 2) == 0) {
 #pragma unroll
     for (int i = 0; i < NW / 4; ++i) kr[i] = kp[i];
 #pragma unroll
@@ -250,44 +254,41 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   }
   __builtin_amdgcn_sched_barrier(0);
 
-  // 1. rotary of the G query heads (and, in the chunk holding p, of the new key), k_rope_qk's
-  //    arithmetic: q*cos + cat(-x2, x1)*sin with every torch op rounded to the storage dtype
+  // 1. rotary of this workgroup's query head (and, in the chunk holding p, of the new key),
+  //    k_rope_qk's arithmetic: q*cos + cat(-x2, x1)*sin with every torch op rounded to the
+  //    storage dtype.  The G workgroups of one kv head all rotate the new key (bit-identical
+  //    values); the first of them writes the cache rows.
   auto rope = [&](float u1, float u2, float &lo, float &hi) {
     lo = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(u1, c1)), round_dt<DT>(__fmul_rn(-u2, s1)))));
     hi = from_bits<DT>(bits_dt<DT>(__fadd_rn(round_dt<DT>(__fmul_rn(u2, c2)), round_dt<DT>(__fmul_rn(u1, s2)))));
   };
-  if (do_q) {
+  const bool mine = p >= j0 && p < j0 + kAttnChunk && p < L;  // this chunk holds the new token
+  if (rt) {
     float lo, hi;
     rope(x1, x2, lo, hi);
-    s_q[gq][dq] = lo;
-    s_q[gq][dq + H2] = hi;
-  }
-  if (do_q2) {  // G * H2 > 256 (D = 128, G > 4): dq2 == dq, so this thread's cos / sin apply
-    float lo, hi;
-    rope(y1, y2, lo, hi);
-    s_q[gq2][dq2] = lo;
-    s_q[gq2][dq2 + H2] = hi;
-  }
-  const bool mine = p >= j0 && p < j0 + kAttnChunk && p < L;  // this chunk holds the new token
-  if (mine && t < H2) {  // t < H2: dr == t
-    float lo, hi;
-    rope(k1, k2, lo, hi);
-    char *kd = reinterpret_cast<char *>(a.kc) + (crow + p) * D * ES;
-    char *vd = reinterpret_cast<char *>(a.vc) + (crow + p) * D * ES;
-    store_f32<DT>(kd, t, lo);
-    store_f32<DT>(kd, t + H2, hi);
-    reinterpret_cast<uint32_t *>(vd)[t] = vnew;
-    s_vn[t] = vnew;
-    // the rotated k as raw elements: element e in the 16-bit half e % 2 of s_kn[e / 2]
-    reinterpret_cast<uint16_t *>(s_kn)[t] = (uint16_t)bits_dt<DT>(lo);
-    reinterpret_cast<uint16_t *>(s_kn)[t + H2] = (uint16_t)bits_dt<DT>(hi);
+    s_q[t] = lo;
+    s_q[t + H2] = hi;
+    if (mine) {
+      rope(k1, k2, lo, hi);
+      if (gq == 0) {
+        char *kd = reinterpret_cast<char *>(a.kc) + (crow + p) * D * ES;
+        char *vd = reinterpret_cast<char *>(a.vc) + (crow + p) * D * ES;
+        store_f32<DT>(kd, t, lo);
+        store_f32<DT>(kd, t + H2, hi);
+        reinterpret_cast<uint32_t *>(vd)[t] = vnew;
+      }
+      s_vn[t] = vnew;
+      // the rotated k as raw elements: element e in the 16-bit half e % 2 of s_kn[e / 2]
+      reinterpret_cast<uint16_t *>(s_kn)[t] = (uint16_t)bits_dt<DT>(lo);
+      reinterpret_cast<uint16_t *>(s_kn)[t + H2] = (uint16_t)bits_dt<DT>(hi);
+    }
   }
   __syncthreads();
   if constexpr ((kAttnAbl & 32) != 0) {
     if (t < 2 * H2) { float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < NW / 4; ++i) acc += __uint_as_float(kr[i].x ^ vr[i].y);
-      reinterpret_cast<float *>(a.out)[t] = acc + s_q[0][t & (D - 1)]; }
+      reinterpret_cast<float *>(a.out)[t] = acc + s_q[t & (D - 1)]; }
     return;
   }
 
@@ -295,6 +296,12 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   //    and stages that half of the position's v row in LDS (zeros where masked / past L)
   {
     const bool ok = mk != 0;
+    if (!spec && ok && j != p) {  // long cache: the rows the mask keeps, read now
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) kr[i] = kp[i];
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) vr[i] = vp[i];
+    }
     uint32_t kw[NW], vw[NW];
     if (ok && j == p) {
 #pragma unroll
@@ -313,80 +320,77 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
     if (half == 0) s_ok[pos_i] = ok ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < NW; ++i) s_v[pos_i][half * NW + i] = vw[i];
-    for (int g = 0; g < ((kAttnAbl & 8) ? 0 : G); ++g) {
-      const float *qg = &s_q[g][half * H2];
+    if constexpr ((kAttnAbl & 8) == 0) {
+      const float *qh = &s_q[half * H2];
       float acc0 = 0.0f, acc1 = 0.0f;  // two chains: even / odd words
 #pragma unroll
       for (int i = 0; i < NW; i += 2) {
-        acc0 = fmaf(from_bits<DT>(kw[i]), qg[2 * i], acc0);
-        acc0 = fmaf(from_bits<DT>(kw[i] >> 16), qg[2 * i + 1], acc0);
-        acc1 = fmaf(from_bits<DT>(kw[i + 1]), qg[2 * i + 2], acc1);
-        acc1 = fmaf(from_bits<DT>(kw[i + 1] >> 16), qg[2 * i + 3], acc1);
+        acc0 = fmaf(from_bits<DT>(kw[i]), qh[2 * i], acc0);
+        acc0 = fmaf(from_bits<DT>(kw[i] >> 16), qh[2 * i + 1], acc0);
+        acc1 = fmaf(from_bits<DT>(kw[i + 1]), qh[2 * i + 2], acc1);
+        acc1 = fmaf(from_bits<DT>(kw[i + 1] >> 16), qh[2 * i + 3], acc1);
       }
-      s_sc[half][g][pos_i] = __fadd_rn(acc0, acc1);
+      s_sc[half][pos_i] = __fadd_rn(acc0, acc1);
     }
   }
   __syncthreads();
 
-  // 3. softmax statistics: 32 threads per query head, 4 positions each; probabilities to s_p
-  //    (their own buffer: no barrier between the score reads and the probability writes)
-  {
-    const int g = t >> 5, i = t & 31;
-    const int gg = g < G ? g : 0;
-    float s[4], m = -INFINITY;
+  // 3. softmax statistics of the chunk: wave 0, two positions per lane
+  if (t < kWave) {
+    float s[2], m = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int pi = 4 * i + r;
-      s[r] = s_ok[pi] ? __fmul_rn(__fadd_rn(s_sc[0][gg][pi], s_sc[1][gg][pi]), a.scale) : -INFINITY;
+    for (int r = 0; r < 2; ++r) {
+      const int pi = 2 * t + r;
+      s[r] = s_ok[pi] ? __fmul_rn(__fadd_rn(s_sc[0][pi], s_sc[1][pi]), a.scale) : -INFINITY;
       m = fmaxf(m, s[r]);
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
-    float l = 0.0f, e[4];
+    for (int o = kWave / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+    float l = 0.0f, e[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 2; ++r) {
       e[r] = s[r] == -INFINITY ? 0.0f : ((kAttnAbl & 16) ? s[r] - m : expf(s[r] - m));
       l += e[r];
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, kWave);
-    if (g < G) {
-      *reinterpret_cast<float4 *>(&s_p[g][4 * i]) = make_float4(e[0], e[1], e[2], e[3]);
-      if (i == 0) { s_m[g] = m; s_l[g] = l; }
-    }
+    for (int o = kWave / 2; o > 0; o >>= 1) l += __shfl_xor(l, o, kWave);
+    s_p[2 * t] = e[0];
+    s_p[2 * t + 1] = e[1];
+    if (t == 0) { s_ml[0] = m; s_ml[1] = l; }
   }
   __syncthreads();
 
-  // 4. P V: one output pair (2 dims of one query head) per thread and round; 8 positions per
-  //    iteration (one 2 x 16-B probability read), two accumulator chains
-  const int n8 = (min(kAttnChunk, L - j0) + 7) & ~7;   // rows past n are zero in s_v and s_p
-  for (int o = t; o < G * H2; o += 256) {
-    const int g = o / H2, w = o - g * H2;
-    float e0 = 0.0f, e1 = 0.0f, d0 = 0.0f, d1 = 0.0f;
-    for (int q0 = 0; q0 < ((kAttnAbl & 4) ? 0 : n8); q0 += 8) {
-      const float4 pa = *reinterpret_cast<const float4 *>(&s_p[g][q0]);
-      const float4 pb = *reinterpret_cast<const float4 *>(&s_p[g][q0 + 4]);
-      const float pr[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-#pragma unroll
-      for (int r = 0; r < 8; r += 2) {
-        const uint32_t va = s_v[q0 + r][w], vb2 = s_v[q0 + r + 1][w];
-        e0 = fmaf(pr[r], from_bits<DT>(va), e0);
-        e1 = fmaf(pr[r], from_bits<DT>(va >> 16), e1);
-        d0 = fmaf(pr[r + 1], from_bits<DT>(vb2), d0);
-        d1 = fmaf(pr[r + 1], from_bits<DT>(vb2 >> 16), d1);
+  // 4. P V: wave w takes positions [32 w, 32 w + 32), lane group ps of the wave every NSUB-th of
+  //    them, lane pl one output pair; the 4 * NSUB slice partials meet in LDS
+  {
+    const int w = t / kWave, lane = t & (kWave - 1), pl = lane % H2, ps = lane / H2;
+    const int n = min(kAttnChunk, L - j0);
+    float e0 = 0.0f, e1 = 0.0f;
+    if constexpr ((kAttnAbl & 4) == 0) {
+      const int q_end = min(32 * w + 32, n);
+#pragma unroll 4
+      for (int q = 32 * w + ps; q < q_end; q += NSUB) {
+        const float pr = s_p[q];
+        const uint32_t vv = s_v[q][pl];
+        e0 = fmaf(pr, from_bits<DT>(vv), e0);
+        e1 = fmaf(pr, from_bits<DT>(vv >> 16), e1);
       }
     }
-    const float acc0 = __fadd_rn(e0, d0), acc1 = __fadd_rn(e1, d1);
+    s_pv[w * NSUB + ps][2 * pl] = e0;
+    s_pv[w * NSUB + ps][2 * pl + 1] = e1;
+  }
+  __syncthreads();
+  if (t < D) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4 * NSUB; ++i) acc += s_pv[i][t];
     if (a.nsplit == 1) {
-      const float inv_l = s_l[g];
-      char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)(h * G + g) * D) * ES;
-      store_f32<DT>(ob, 2 * w, __fdiv_rn(acc0, inv_l));
-      store_f32<DT>(ob, 2 * w + 1, __fdiv_rn(acc1, inv_l));
+      char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)hq * D) * ES;
+      store_f32<DT>(ob, t, __fdiv_rn(acc, s_ml[1]));
     } else {
-      float *pp = a.part + ((((long long)b * a.Hkv + h) * a.nsplit + split) * G + g) * (D + 2);
-      pp[2 * w] = acc0;
-      pp[2 * w + 1] = acc1;
-      if (w == 0) { pp[D] = s_m[g]; pp[D + 1] = s_l[g]; }
+      float *pp = a.part + ((((long long)b * a.Hkv + h) * a.nsplit + split) * G + gq) * (D + 2);
+      pp[t] = acc;
+      if (t == 0) { pp[D] = s_ml[0]; pp[D + 1] = s_ml[1]; }
     }
   }
 
@@ -427,7 +431,7 @@ __global__ __launch_bounds__(256) void k_decode_attn_combine(DecodeAttnArgs a) {
 
 template <int DT, int D>
 void launch_decode_attn(const DecodeAttnArgs &a, int B, hipStream_t s) {
-  hipLaunchKernelGGL((k_decode_attn<DT, D>), dim3(a.nsplit, a.Hkv, B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_decode_attn<DT, D>), dim3(a.nsplit, a.Hkv * a.G, B), dim3(256), 0, s, a);
   if (a.nsplit > 1) hipLaunchKernelGGL((k_decode_attn_combine<DT, D>), dim3(a.Hkv, B), dim3(256), 0, s, a);
 }
 
@@ -538,7 +542,7 @@ extern "C" int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int
   if (B < 0 || Hq < 0 || Hkv < 0 || D < 0 || L < 0) return QZ_ERR_ARG;
   if (B == 0 || Hq == 0) return 0;
   if (Hkv == 0 || Hq % Hkv != 0 || Hq / Hkv > kAttnMaxG || (D != 64 && D != 128) || L == 0) return QZ_ERR_SHAPE;
-  if (B > 65535 || Hkv > 65535) return QZ_ERR_SHAPE;
+  if (B > 65535 || Hq > 65535) return QZ_ERR_SHAPE;
   if (!q || !k || !v || !cos || !sin || !k_cache || !v_cache || !mask || !pos || !arrive || !out) return QZ_ERR_ARG;
   if (q_row < (long long)Hq * D || k_row < (long long)Hkv * D || v_row < (long long)Hkv * D || cs_row < 0 ||
       out_row < (long long)Hq * D)

@@ -191,6 +191,15 @@ template <int DT> __device__ __forceinline__ float from_bits(uint32_t u) {
   else return __uint_as_float(u << 16);
 }
 
+template <int DT> __device__ __forceinline__ float dot2_dt(uint32_t a, uint32_t b, float c) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+  if constexpr (DT == QZ_DT_F16)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c, false);
+  else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b16x2, a), __builtin_bit_cast(b16x2, b), c, false);
+}
+
 template <int DT, int D>
 __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   constexpr int H2 = D / 2;      // rotary half; also the share of a row one thread dots
   constexpr int NW = H2 / 2;     // 32-bit words of half a row
   constexpr int NSUB = kWave / H2;  // P V: lane groups per wave (D = 128: 1, D = 64: 2)
-  __shared__ float s_q[D];                             // rotated q (storage-rounded values)
+  __shared__ uint32_t s_qh[H2];                        // rotated q, raw (the layout of s_kn)
   __shared__ float s_sc[2][kAttnChunk];                // half-row partial scores
   __shared__ float s_p[kAttnChunk];                    // probabilities (0: masked / past L)
   __shared__ uint32_t s_v[kAttnChunk][H2];             // raw v rows (zero where masked)
@@ -266,8 +275,8 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   if (rt) {
     float lo, hi;
     rope(x1, x2, lo, hi);
-    s_q[t] = lo;
-    s_q[t + H2] = hi;
+    reinterpret_cast<uint16_t *>(s_qh)[t] = (uint16_t)bits_dt<DT>(lo);
+    reinterpret_cast<uint16_t *>(s_qh)[t + H2] = (uint16_t)bits_dt<DT>(hi);
     if (mine) {
       rope(k1, k2, lo, hi);
       if (gq == 0) {
@@ -288,7 +297,7 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
     if (t < 2 * H2) { float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < NW / 4; ++i) acc += __uint_as_float(kr[i].x ^ vr[i].y);
-      reinterpret_cast<float *>(a.out)[t] = acc + s_q[t & (D - 1)]; }
+      reinterpret_cast<float *>(a.out)[t] = acc + __uint_as_float(s_qh[t & (H2 - 1)]); }
     return;
   }
 
@@ -321,14 +330,13 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
 #pragma unroll
     for (int i = 0; i < NW; ++i) s_v[pos_i][half * NW + i] = vw[i];
     if constexpr ((kAttnAbl & 8) == 0) {
-      const float *qh = &s_q[half * H2];
+      // both operands are storage-dtype values: v_dot2 of the raw pairs, products exact in fp32
+      const uint32_t *qw = &s_qh[half * NW];
       float acc0 = 0.0f, acc1 = 0.0f;  // two chains: even / odd words
 #pragma unroll
       for (int i = 0; i < NW; i += 2) {
-        acc0 = fmaf(from_bits<DT>(kw[i]), qh[2 * i], acc0);
-        acc0 = fmaf(from_bits<DT>(kw[i] >> 16), qh[2 * i + 1], acc0);
-        acc1 = fmaf(from_bits<DT>(kw[i + 1]), qh[2 * i + 2], acc1);
-        acc1 = fmaf(from_bits<DT>(kw[i + 1] >> 16), qh[2 * i + 3], acc1);
+        acc0 = dot2_dt<DT>(kw[i], qw[i], acc0);
+        acc1 = dot2_dt<DT>(kw[i + 1], qw[i + 1], acc1);
       }
       s_sc[half][pos_i] = __fadd_rn(acc0, acc1);
     }
@@ -364,12 +372,13 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   //    them, lane pl one output pair; the 4 * NSUB slice partials meet in LDS
   {
     const int w = t / kWave, lane = t & (kWave - 1), pl = lane % H2, ps = lane / H2;
-    const int n = min(kAttnChunk, L - j0);
     float e0 = 0.0f, e1 = 0.0f;
     if constexpr ((kAttnAbl & 4) == 0) {
-      const int q_end = min(32 * w + 32, n);
-#pragma unroll 4
-      for (int q = 32 * w + ps; q < q_end; q += NSUB) {
+      // a fixed trip count, fully unrolled (every LDS read issued before the FMAs wait): rows
+      // past L are zero in s_v and s_p
+#pragma unroll
+      for (int i = 0; i < 32 / NSUB; ++i) {
+        const int q = 32 * w + ps + NSUB * i;
         const float pr = s_p[q];
         const uint32_t vv = s_v[q][pl];
         e0 = fmaf(pr, from_bits<DT>(vv), e0);

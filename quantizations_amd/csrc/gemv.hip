@@ -48,6 +48,8 @@
 // the output.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace qz {
 
 enum {
@@ -1770,6 +1772,14 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
   if (WK != 1 || R < 2) return QZ_ERR_SHAPE;
+  // QZ_PAIR_R (measurement knob, read once): rows per wave for the pair launch (2, 3, 4, 6, 8); the per-row
+  // sums do not depend on R, so neither do the bits
+  static const int pair_r = [] {
+    const char *e = getenv("QZ_PAIR_R");
+    const int v = e ? atoi(e) : 0;
+    return v == 2 || v == 3 || v == 4 || v == 6 || v == 8 ? v : 0;
+  }();
+  if (pair_r) R = pair_r;
   const int blocks = (M + 2 * R - 1) / (2 * R);
   if (norm_weight && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
   for (int i = 2; i < kMaxSeg; ++i) g.start[i] = 0;
@@ -1780,6 +1790,9 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
 #define QZ_PS_R(DQ_, DT_, CL_, NRM_)           \
   do {                                          \
     if (R == 4) QZ_PS(DQ_, DT_, 4, CL_, NRM_);  \
+    else if (R == 8) QZ_PS(DQ_, DT_, 8, CL_, NRM_);  \
+    else if (R == 6) QZ_PS(DQ_, DT_, 6, CL_, NRM_);  \
+    else if (R == 3) QZ_PS(DQ_, DT_, 3, CL_, NRM_);  \
     else QZ_PS(DQ_, DT_, 2, CL_, NRM_);         \
   } while (0)
 #define QZ_PS_N(DQ_, DT_, CL_)                                                      \

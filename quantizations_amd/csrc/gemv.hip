@@ -1659,13 +1659,13 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   int R, WK;
   choose_geometry((int)total_m, K, dtype, &R, &WK);
   // QZ_GROUPED_NORM_R (measurement knob, read once): rows per wave of the fused pre-norm launch
-  // (1, 2, 4; whole rows per wave)
+  // (1, 2, 4) where the geometry keeps whole rows per wave (WK = 1: the same per-row sums)
   static const int norm_r = [] {
     const char *e = getenv("QZ_GROUPED_NORM_R");
     const int v = e ? atoi(e) : 0;
     return v == 1 || v == 2 || v == 4 ? v : 0;
   }();
-  if (nw && norm_r) { R = norm_r; WK = 1; }
+  if (nw && norm_r && WK == 1) R = norm_r;
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {

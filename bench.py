@@ -1102,6 +1102,13 @@ def main():
     layer = None
     if not args.no_roofline:
         layer = rowsplit_layer(rank, world, sharded, gatherer=gatherer)   # every rank takes part (the all-gather)
+    if gatherer is not None and gatherer.failed_anywhere():
+        # a one-shot exchange gave up waiting for a peer (5 s bound): its outputs, and so the
+        # measured decode, are not valid -- no line is reported (every rank takes this branch)
+        log(f"[rank {rank}] error: a one-shot all-gather timed out on some rank; the measurement is invalid")
+        dist.barrier()
+        dist.destroy_process_group()
+        sys.exit(4)
 
     prefill = None
     if rank == 0 and world == 1 and not args.no_prefill:

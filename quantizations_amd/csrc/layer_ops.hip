@@ -393,6 +393,9 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < 4 * NSUB; ++i) acc += s_pv[i][t];
+    // a full cache (p >= L) has no slot for the new token: HF's StaticLayer.update fails on the
+    // out-of-range index_copy_; here the output is NaN (never a silently stale attention)
+    if (p >= L) acc = __builtin_nanf("");
     if (a.nsplit == 1) {
       char *ob = reinterpret_cast<char *>(a.out) + ((long long)b * a.os + (long long)hq * D) * ES;
       store_f32<DT>(ob, t, __fdiv_rn(acc, s_ml[1]));
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   if (t == 0 && (kAttnAbl & 1) == 0) {
     const unsigned int total = gridDim.x * gridDim.y * gridDim.z;
     if (atomicAdd(a.arrive, 1u) == total - 1u) {
-      *a.pos = p + 1;
+      if (p < L) *a.pos = p + 1;   // a full cache keeps its position (every later call is NaN too)
       atomicExch(a.arrive, 0u);
     }
   }

@@ -39,31 +39,51 @@ class OneShotAllGather:
             raise ValueError("OneShotAllGather supports up to 8 ranks (one MI355X node)")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.slot_bytes = int(slot_bytes)
-        nbytes = int(lib.qz_exchange_bytes(self.world, self.slot_bytes))
-        own = ctypes.c_void_p()
-        check(lib.qz_exchange_alloc(nbytes, ctypes.byref(own)), "qz_exchange_alloc")
-        self._own = own
+        self._own = None
         self._opened = []
-        hsz = int(lib.qz_ipc_handle_size())
-        handle = (ctypes.c_char * hsz)()
-        check(lib.qz_ipc_get_handle(own, handle), "qz_ipc_get_handle")
-        mine = (bytes(handle), self.device.index)
+        # Every rank reaches the same collectives in the same order whatever fails locally: a
+        # local error is carried into the exchange of handles and the MIN vote below, and then
+        # raised on EVERY rank (never on one rank while the others wait in a collective).
+        err = None
+        mine = None
+        try:
+            nbytes = int(lib.qz_exchange_bytes(self.world, self.slot_bytes))
+            own = ctypes.c_void_p()
+            check(lib.qz_exchange_alloc(nbytes, ctypes.byref(own)), "qz_exchange_alloc")
+            self._own = own
+            hsz = int(lib.qz_ipc_handle_size())
+            handle = (ctypes.c_char * hsz)()
+            check(lib.qz_ipc_get_handle(own, handle), "qz_ipc_get_handle")
+            mine = (bytes(handle), self.device.index)
+        except Exception as e:  # noqa: BLE001 -- re-raised after the vote
+            err = e
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=group)
         peers = (ctypes.c_void_p * self.world)()
-        for r, (h, dev) in enumerate(allh):
-            if r == self.rank:
-                peers[r] = own.value
-                continue
-            check(lib.qz_enable_peer_access(int(dev)), f"qz_enable_peer_access({dev})")
-            p = ctypes.c_void_p()
-            check(lib.qz_ipc_open_handle(ctypes.create_string_buffer(h, hsz), ctypes.byref(p)),
-                  f"qz_ipc_open_handle(rank {r})")
-            self._opened.append(p)
-            peers[r] = p.value
+        if err is None:
+            try:
+                if any(h is None for h in allh):
+                    raise RuntimeError("a peer could not create its exchange buffer")
+                for r, (h, dev) in enumerate(allh):
+                    if r == self.rank:
+                        peers[r] = self._own.value
+                        continue
+                    check(lib.qz_enable_peer_access(int(dev)), f"qz_enable_peer_access({dev})")
+                    p = ctypes.c_void_p()
+                    check(lib.qz_ipc_open_handle(ctypes.create_string_buffer(h, hsz), ctypes.byref(p)),
+                          f"qz_ipc_open_handle(rank {r})")
+                    self._opened.append(p)
+                    peers[r] = p.value
+            except Exception as e:  # noqa: BLE001 -- re-raised after the vote
+                err = e
         self._peers = peers
         self.epoch = torch.zeros(2, dtype=torch.int32, device=self.device)   # epoch, last-finisher ticket
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        ok = torch.tensor([int(err is None)], dtype=torch.int32, device=self.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if not ok.item():
+            self.close()
+            raise RuntimeError(f"one-shot all-gather setup failed on some rank (here: {err!r})")
         dist.barrier(group=group)   # every rank has mapped every buffer before the first launch
 
     def accepts(self, inp: torch.Tensor) -> bool:
@@ -88,6 +108,12 @@ class OneShotAllGather:
         """True if any launch so far timed out waiting for a peer (synchronises)."""
         return bool(self.status.item())
 
+    def failed_anywhere(self) -> bool:
+        """failed() on ANY rank of the group (a collective: every rank must call it)."""
+        flag = torch.tensor([int(self.failed())], dtype=torch.int32, device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        return bool(flag.item())
+
     def verify(self, sizes=(256, 2048, 14336), dtype=torch.float16) -> bool:
         """Compare with dist.all_gather_into_tensor on this group for a few payload sizes
         (elements), twice each (both slot parities).  True if every result is identical."""
@@ -101,9 +127,12 @@ class OneShotAllGather:
                 b = torch.empty(self.world * n, device=self.device, dtype=dtype)
                 dist.all_gather_into_tensor(b, x, group=self.group)
                 for mode in (0, 1, 2):
-                    a = torch.empty_like(b)
-                    self(a, x, mode)
-                    ok = ok and bool(torch.equal(a, b))
+                    try:   # a local failure must not skip this rank's later collectives
+                        a = torch.empty_like(b)
+                        self(a, x, mode)
+                        ok = ok and bool(torch.equal(a, b))
+                    except Exception:  # noqa: BLE001 -- reported by the vote below
+                        ok = False
         flag = torch.tensor([int(ok and not self.failed())], device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item())

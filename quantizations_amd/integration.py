@@ -308,7 +308,8 @@ def _fused_attention_forward(mod: nn.Module, orig):
                 k = mod.k_proj(hidden_states)
                 v = mod.v_proj(hidden_states)
                 if q.shape[-1] != nq * mod.head_dim or k.shape[-1] != layer.keys.shape[1] * mod.head_dim:
-                    return orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+                    h, w = orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
+                    return (h if _qz_residual is None else _qz_residual + h), w
                 out = decode_attention(q, k, v, cos, sin, layer.keys, layer.values, attention_mask,
                                        layer.cumulative_length, arrive, nq, mod.scaling)
                 return _project(mod.o_proj, out, _qz_residual), None

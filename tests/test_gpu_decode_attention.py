@@ -94,6 +94,24 @@ def test_decode_attention_matches_rope_cache_update_and_softmax(dtype, B, Hq, Hk
     torch.testing.assert_close(out.double(), ref, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("L", [112, 300])   # one chunk / three chunks (the combine launch)
+def test_decode_attention_full_cache_is_loud(L):
+    """One token past max_cache_len: HF's StaticLayer.update fails on the out-of-range
+    index_copy_; the fused launch has no slot either, so its output is NaN, the cache is
+    untouched and the position stays at L (never a silently stale output)."""
+    from quantizations_amd.layer_ops import decode_attention
+
+    q, k, v, cos, sin, kc, vc, mask, pos = _case(1, 32, 8, 128, L, L - 1, torch.float16, seed=11)
+    pos.fill_(L)
+    kc0, vc0 = kc.clone(), vc.clone()
+    arrive = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = decode_attention(q, k, v, cos, sin, kc, vc, mask, pos, arrive, 32, 1.0 / math.sqrt(128))
+    torch.cuda.synchronize()
+    assert torch.isnan(out).all()
+    assert torch.equal(kc, kc0) and torch.equal(vc, vc0)
+    assert int(pos) == L and int(arrive) == 0
+
+
 def test_decode_attention_consecutive_steps_and_sdpa():
     """Two steps in a row (the arrival counter and the position carry over) and the same
     output as torch's own SDPA on the updated cache within fp16 flash-attention tolerance."""

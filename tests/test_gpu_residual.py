@@ -105,3 +105,42 @@ def test_llama_residual_decoder_bit_identical_eager_and_graph():
             assert all(torch.equal(a, b) for a, b in zip(got_graph, ref))
     finally:
         unfuse_layer_ops(model)
+
+
+def test_fused_attention_fallback_keeps_the_residual():
+    """The residual-fused decoder passes `residual` into the patched attention; when that
+    attention cannot take the one-launch path (here: a q width that disagrees with the head
+    count the cache implies) its fallback must still return residual + attention (ADVICE r3:
+    the early return dropped it).  Logits vs the unfused transformers model."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    from transformers.cache_utils import StaticCache
+
+    from quantizations_amd.integration import fuse_layer_ops, replace_with_bnb_linear, unfuse_layer_ops
+
+    cfg = LlamaConfig(hidden_size=1024, intermediate_size=2048, num_hidden_layers=2, num_attention_heads=8,
+                      num_key_value_heads=2, vocab_size=512)
+    torch.manual_seed(5)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, quant_type="nf4", compute_dtype=torch.float32)
+    ids = torch.randint(0, 512, (1, 9), device=DEV, generator=torch.Generator(device="cuda").manual_seed(2))
+
+    def decode():
+        cache = StaticCache(config=cfg, max_cache_len=32)
+        out = model(input_ids=ids, past_key_values=cache, cache_position=torch.arange(9, device=DEV))
+        tok = out.logits[:, -1:].argmax(-1)
+        pos = torch.tensor([9], device=DEV)
+        lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos.view(1, 1)).logits
+        torch.cuda.synchronize()
+        return lo[:, -1].float()
+
+    with torch.no_grad():
+        ref = decode()
+        try:
+            fuse_layer_ops(model)   # residual-fused decoder + one-launch attention
+            assert sum("_qz_residual_decoder" in m.__dict__ for m in model.modules()) == cfg.num_hidden_layers
+            model.config.num_attention_heads = 16   # the fused path's head count no longer fits q
+            got = decode()
+        finally:
+            model.config.num_attention_heads = 8
+            unfuse_layer_ops(model)
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)

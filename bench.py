@@ -231,7 +231,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
                                      residual=residual, mlp_pair=mlp_pair)  # one launch each
-    if prenorm and fuse and not sharded and layer_ops in ("all", "norm"):
+    if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
     return n_groups, n_layer_ops
@@ -1086,7 +1086,7 @@ def main():
                                                                     * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
                 "dominant_decode_kernel": dominant_roofline(
-                    prenorm=bool(not args.no_prenorm and not sharded and not args.no_fuse
+                    prenorm=bool(not args.no_prenorm and not args.no_fuse
                                  and layer_ops in ("all", "norm")),
                     pair=bool(not args.no_mlp_pair and not args.no_fuse and layer_ops in ("all", "all+decoder", "mlp")))}
         from quantizations_amd import _lib, core
@@ -1142,7 +1142,7 @@ def main():
             "roofline": roof, "parity": parity, "cpu_baseline": cpu, "prefill_config4": prefill,
         }
         line["config"]["compute_dtype"] = args.compute_dtype
-        line["config"]["rmsnorm_in_grouped_gemv"] = bool(not args.no_prenorm and not sharded and not args.no_fuse
+        line["config"]["rmsnorm_in_grouped_gemv"] = bool(not args.no_prenorm and not args.no_fuse
                                                          and layer_ops in ("all", "norm"))
         line["config"]["decode_attention"] = ("qz_decode_attention" if not args.no_attention
                                               and layer_ops in ("all", "all+decoder") else "transformers sdpa")

@@ -448,14 +448,15 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
 
 
 def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> Optional[Tensor]:
-    """F.silu(gate) * up for items = [(B, state, bias)] of gate_proj and up_proj (equal shapes)
-    and a single-token A, in ONE launch (qz_gemv_4bit_pair_silu): bit-identical to
-    gemv_4bit_grouped + layer_ops.silu_mul.  norm=(weight, eps) as in gemv_4bit_grouped.
-    Returns None for what the kernel does not take (the caller runs the two launches)."""
-    items = list(items)
+    """F.silu(gate) * up for items = [(B, state, bias[, block_base])] of gate_proj and up_proj
+    (equal shapes; block_base for row shards, parallel.sharded_silu_pair) and a single-token A,
+    in ONE launch (qz_gemv_4bit_pair_silu): bit-identical to gemv_4bit_grouped +
+    layer_ops.silu_mul.  norm=(weight, eps) as in gemv_4bit_grouped.  Returns None for what
+    the kernel does not take (the caller runs the two launches)."""
+    items = [tuple(it) + (0,) * (4 - len(it)) for it in items]
     if len(items) != 2 or A.numel() != A.shape[-1] or A.dtype not in (torch.float16, torch.bfloat16):
         return None
-    (B0, s0, b0), (B1, s1, b1) = items
+    s0, s1 = items[0][1], items[1][1]
     K = s0.shape[1]
     if (A.shape[-1] != K or s1.shape != s0.shape or s1.quant_type != s0.quant_type or s1.blocksize != s0.blocksize
             or s1.nested != s0.nested or (s0.nested and s1.state2.blocksize != s0.state2.blocksize)):
@@ -463,11 +464,11 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     A = A.contiguous()
     M = s0.shape[0]
     segs = (_lib.GemvSegment * 2)()
-    for i, (B, st, bias) in enumerate(items):
+    for i, (B, st, bias, block_base) in enumerate(items):
         if bias is not None and bias.dtype != A.dtype:
             bias = bias.to(A.dtype)
         am, qam, am2, code2, off, _ = st.scale_args()
-        segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, 0, ptr(bias), None)
+        segs[i] = _lib.GemvSegment(M, ptr(B), am, qam, am2, code2, off, int(block_base), ptr(bias), None)
     shape = (A.shape[0], A.shape[1], M) if A.dim() == 3 else (A.shape[0], M) if A.dim() == 2 else (M,)
     h = torch.empty(shape, dtype=A.dtype, device=A.device)
     nw, eps = (None, 0.0) if norm is None else norm

@@ -225,6 +225,7 @@ struct GemvParams {
   int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12), 2 = exact NF4 (CL) precomputed byte table;
                      // lut != nullptr builds an exact (CL) table in kernel
   uint32_t tab[8];
+  uint32_t tab_lo[8];  // exact codes (CL): fp16 byte planes of the lo parts (the hi parts are tab)
   const void *nw;    // fused pre-norm (NRM): the RMSNorm weight [K], or nullptr
   float eps;         //   and its epsilon
   const void *res;   // residual [M] added after the output rounding (y = round(round(x W^T) + res)), or nullptr
@@ -320,6 +321,8 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   p.res = keep_sp(in.res);
 #pragma unroll
   for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p.tab_lo[i] = keep_s(in.tab_lo[i]);
   p.nw = keep_sp(in.nw);
   p.eps = keep_s(in.eps);
   return p;
@@ -585,6 +588,57 @@ __device__ __forceinline__ float chunk_dot_tab_f32(const u32x4 &wv, const uint32
   return s0 + s1;
 }
 
+// Exact codes by mixed-precision FMA (FM, round 4): the byte table holds the two codes as fp32
+// (the kRawF32 table: the reference's fp32 quant_map values, kernels.cu:1115-1120) and each
+// goes into one v_fma_mix_f32 with its raw fp16 activation, the half picked by op_sel -- no x
+// conversion, no hi/lo code split.  Per packed byte: one ds_read_b64 and two full-rate FMAs
+// (the hi + lo table needs two half-rate v_dot2c).  The products are fp32 (an fp16 x an fp32
+// code, rounded once), as the reference's fp32 FMA chain (kernels.cu:1169-1210).
+// Addresses: AD = 0 builds (byte << 7) | jb with two VALU (the 16-copy, 128-B-entry table);
+// AD = 1 is the 256-B-entry table (WT: 32 bank-private copies, no conflicts) addressed by ONE
+// v_mov_b32_sdwa that writes the byte into bits 8..15 of a register whose byte 0 holds the
+// lane's copy offset jb for the whole kernel (`ad`, initialised once; bytes 2-3 stay zero).
+template <int M_> __device__ __forceinline__ void sdwa_byte1(uint32_t &a, uint32_t w) {
+  if constexpr (M_ == 0) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(a) : "v"(w));
+  else if constexpr (M_ == 1) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(a) : "v"(w));
+  else if constexpr (M_ == 2) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(w));
+  else asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(a) : "v"(w));
+}
+template <int AD>
+__device__ __forceinline__ float chunk_dot_tab_fm(const u32x4 &wv, const uint32_t (&xr)[16], const uint32_t *s_tab,
+                                                  uint32_t jb, uint32_t (&ad)[16]) {
+  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t a[4];
+    if constexpr (AD == 1) {
+      sdwa_byte1<0>(ad[4 * d + 0], w[d]);
+      sdwa_byte1<1>(ad[4 * d + 1], w[d]);
+      sdwa_byte1<2>(ad[4 * d + 2], w[d]);
+      sdwa_byte1<3>(ad[4 * d + 3], w[d]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = ad[4 * d + m];
+    } else {
+      a[0] = ((w[d] << 7) & 0x7F80u) | jb;
+      a[1] = ((w[d] >> 1) & 0x7F80u) | jb;
+      a[2] = ((w[d] >> 9) & 0x7F80u) | jb;
+      a[3] = ((w[d] >> 17) & 0x7F80u) | jb;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a[m]);
+      const uint32_t xv = xr[4 * d + m];   // x[2j] in the low half, x[2j + 1] in the high half
+      // written out: left to itself hipcc SLP-packs the scalar FMAs into v_pk_fma_f32 fed by
+      // v_cvt_f32_f16 + v_mov copies (twice the VALU)
+      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(s[(2 * m) & 3]) : "v"(xv), "v"(e.x));
+      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(s[(2 * m + 1) & 3]) : "v"(xv), "v"(e.y));
+    }
+  }
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
 // (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
 // readlane round trips through SGPRs.
@@ -827,7 +881,7 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false>
+          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
                                           const GemvParams *pair = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
@@ -850,6 +904,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   constexpr bool kBF = XSlice<MODE, DT>::kRawBF;
   constexpr bool kF32 = XSlice<MODE, DT>::kRawF32;    // fp32 x: fp32 code table, v_fma_f32
   constexpr bool kWide = CL || kBF || kF32;
+  // FMV (exact codes, fp16 x): 0 = hi + lo fp16 code pairs by v_dot2c; 1 = fp32 codes by
+  // v_fma_mix_f32 (chunk_dot_tab_fm), two-VALU addresses; 2 = the same on the 256-B-entry (WT)
+  // table with one-SDWA addresses
+  constexpr bool kFM = CL && DT == QZ_DT_F16 && FMV != 0;
+  static_assert(FMV != 2 || WT, "SDWA addresses index the 256-B-entry table");
+  // OPT (round 4): bit 0 = issue the wave's second K-step before the prologue barrier (both steps
+  // of a K = 4096 row in flight from the start); bit 1 = build the fp16 byte-table entry from the
+  // SGPR byte planes (tab / tab_lo) instead of loading it (no global load gates the barrier)
+  constexpr bool kEarly = (OPT & 1) != 0;
+  constexpr bool kSTab = (OPT & 2) != 0 && MODE == kModeTab && !kBF && !kF32 && !kFM;
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
@@ -888,7 +952,24 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // 1b. the precomputed byte-table entry of this thread (issued before the
   // weights, so waiting for it does not wait for the first HBM step)
   u32x4 tab_entry = {0u, 0u, 0u, 0u};
-  if constexpr (kNoPro && MODE == kModeTab) {
+  if constexpr (kSTab) {
+    if (!p.lut && threadIdx.x < 256) {
+      uint32_t P[4], tp[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) tp[i] = p.tab[i];
+      decode_lut16((uint32_t)threadIdx.x, tp, P);
+      const uint32_t h = (P[0] & 0xFFFFu) | (P[2] << 16);
+      if constexpr (CL) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tp[i] = p.tab_lo[i];
+        decode_lut16((uint32_t)threadIdx.x, tp, P);
+        const uint32_t l = (P[0] & 0xFFFFu) | (P[2] << 16);
+        tab_entry = u32x4{h, l, h, l};
+      } else {
+        tab_entry = u32x4{h, h, h, h};
+      }
+    }
+  } else if constexpr (kNoPro && MODE == kModeTab) {
     uint32_t P[4], tp[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) tp[i] = p.tab[i];
@@ -898,7 +979,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   } else if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
     if (!p.lut && threadIdx.x < 256) {
-      const ByteTable *bt = kF32  ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
+      const ByteTable *bt = (kF32 || kFM) ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
                             : kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
                                   : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
       tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
@@ -937,10 +1018,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     __builtin_amdgcn_sched_barrier(0);
   }
   // 2. this wave's first step of HBM traffic
-  StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> cur;
+  StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> cur, other;
   int s = wk;
   cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
   const bool have = s < nsteps;
+  const int n_my = have ? (nsteps - wk + WK - 1) / WK : 0;  // this wave's steps: s = wk, wk + WK, ...
+  if constexpr (kEarly) {
+    if (n_my >= 2) other.issue(p, row0, s + WK, lane, row_bytes);
+  }
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
     if (NW * 64 == 256 || threadIdx.x < 256) s_code2[0][threadIdx.x & 255] = c2;
@@ -980,7 +1065,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // runtime codebook (always exact codes) 2^-S of its in-kernel split
   float out_scale = p.out_scale;
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if constexpr (kF32) {
+    if constexpr (kF32 || kFM) {
       if (p.lut) {
         out_scale = 1.0f;
         build_byte_table_f32<NW * 64, kPieces>(s_tab, p.lut);
@@ -1029,6 +1114,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+  uint32_t ad[16];   // FMV = 2: per-byte address registers, byte 0 = jb for the whole kernel
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ad[i] = jb;
 
   // Steady state: the next step's loads are issued UNCONDITIONALLY before the
   // current step is consumed, and the last step is peeled after the loop.  (A
@@ -1059,6 +1147,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       if constexpr (kScaled) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
       if constexpr (kF32) d = chunk_dot_tab_f32(c.wv[r], c.xs.raw, s_tab, jb);
+      else if constexpr (kFM) d = chunk_dot_tab_fm<FMV == 2 ? 1 : 0>(c.wv[r], hi, s_tab, jb, ad);
       else if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
@@ -1070,9 +1159,34 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // register whose load is in flight forces vmcnt(0) -- the prefetch is then
   // waited for before the current step is decoded.  Every consume(cur) below
   // reads the same registers on every path, so no copies are needed.
-  if (have) {
-    const int n = (nsteps - wk + WK - 1) / WK;  // this wave's steps: s = wk, wk + WK, ...
-    Loads other;
+  if (kEarly && have) {
+    // `other` already holds step s + WK (n >= 2); at the loop top cur = step j, other = j + 1
+    const int n = n_my;
+    int j = 0;
+    for (; j + 3 < n; j += 2) {
+      consume(cur);
+      cur.issue(p, row0, s + 2 * WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(other);
+      other.issue(p, row0, s + 3 * WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      s += 2 * WK;
+    }
+    if (n - j == 3) {
+      consume(cur);
+      cur.issue(p, row0, s + 2 * WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(other);
+      consume(cur);
+    } else if (n - j == 2) {
+      consume(cur);
+      QZ_STAMP(2);
+      consume(other);
+    } else {
+      consume(cur);
+    }
+  } else if (have) {
+    const int n = n_my;
     int j = 0;
     for (; j + 2 < n; j += 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
@@ -1187,9 +1301,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false>
+          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT>(p, blockIdx.x);
 }
 
 // Streaming ("persistent") form for rows of exactly NS K-steps (K = 2048 * NS, full-step
@@ -1411,6 +1525,21 @@ static void build_tables(int mode, int quant_type, uint32_t tab[8], float *out_s
   *out_scale = 1.0f;
 }
 
+// Exact NF4 codes (CL) as fp16 byte planes: hi = fp16(c * 2^14) in `hi`, lo = fp16(c * 2^14 - hi)
+// in `lo` (the kernel's SGPR-built table, OPT & 2; the same values as g_byte_tab_nf4x)
+static void build_exact_planes(uint32_t hi[8], uint32_t lo[8]) {
+  for (int i = 0; i < 8; ++i) hi[i] = lo[i] = 0;
+  for (int i = 0; i < 16; ++i) {
+    const float c = kNF4Host[i] * (float)(1 << kNF4ExactShift);
+    const uint16_t h = f32_to_f16_bits(c);
+    const uint16_t l = f32_to_f16_bits(c - __half2float(__ushort_as_half(h)));
+    hi[i >> 2] |= (uint32_t)(h & 0xFF) << (8 * (i & 3));
+    hi[4 + (i >> 2)] |= (uint32_t)(h >> 8) << (8 * (i & 3));
+    lo[i >> 2] |= (uint32_t)(l & 0xFF) << (8 * (i & 3));
+    lo[4 + (i >> 2)] |= (uint32_t)(l >> 8) << (8 * (i & 3));
+  }
+}
+
 static int ilog2(long long v) {
   int l = 0;
   while ((1LL << l) < v) ++l;
@@ -1504,8 +1633,12 @@ static void set_tables(int quant_type, const float *lut, bool cl, int dtype, Gem
     return;
   }
   p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : (cl ? 2 : 0);
+  for (int i = 0; i < 8; ++i) p->tab_lo[i] = 0;
   if (lut) p->out_scale = 1.0f;
-  else if (cl) p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
+  else if (cl) {
+    p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
+    build_exact_planes(p->tab, p->tab_lo);
+  }
 }
 
 // Exact codes: a runtime codebook is always decoded exactly (the reference
@@ -1776,10 +1909,11 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
     return QZ_ERR_SHAPE;
   // the geometry qz_gemv_4bit_grouped takes for the pair's 2M rows (same per-row summation order,
   // so the same bits); the epilogue needs whole rows per wave: splits along K (WK > 1, e.g. the
-  // K = 8192 layers) and single-row waves are left to the two-launch form
+  // K = 8192 layers) are left to the two-launch form.  Single-row waves (R = 1: small row shards,
+  // e.g. Llama-3-8B gate/up over 8 ranks) take the pair launch too
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
-  if (WK != 1 || R < 2) return QZ_ERR_SHAPE;
+  if (WK != 1) return QZ_ERR_SHAPE;
   // QZ_PAIR_R (measurement knob, read once): rows per wave for the pair launch (2, 3, 4, 6, 8); the per-row
   // sums do not depend on R, so neither do the bits
   static const int pair_r = [] {
@@ -1801,6 +1935,7 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
     else if (R == 8) QZ_PS(DQ_, DT_, 8, CL_, NRM_);  \
     else if (R == 6) QZ_PS(DQ_, DT_, 6, CL_, NRM_);  \
     else if (R == 3) QZ_PS(DQ_, DT_, 3, CL_, NRM_);  \
+    else if (R == 1) QZ_PS(DQ_, DT_, 1, CL_, NRM_);  \
     else QZ_PS(DQ_, DT_, 2, CL_, NRM_);         \
   } while (0)
 #define QZ_PS_N(DQ_, DT_, CL_)                                                      \

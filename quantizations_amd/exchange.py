@@ -25,6 +25,14 @@ from . import _lib
 from ._lib import check, lib
 
 
+def _vote(value: int, op, group, device) -> int:
+    """MIN/MAX of an int over the group (the tensor on the CPU for gloo, on the GPU for RCCL)."""
+    dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+    t = torch.tensor([int(value)], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=op, group=group)
+    return int(t.item())
+
+
 class OneShotAllGather:
     """All-gather of up to `slot_bytes` per rank, rank-major output (the order of
     ``dist.all_gather_into_tensor``), through IPC-mapped peer buffers."""
@@ -79,9 +87,7 @@ class OneShotAllGather:
         self._peers = peers
         self.epoch = torch.zeros(2, dtype=torch.int32, device=self.device)   # epoch, last-finisher ticket
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
-        ok = torch.tensor([int(err is None)], dtype=torch.int32, device=self.device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-        if not ok.item():
+        if not _vote(err is None, dist.ReduceOp.MIN, group, self.device):
             self.close()
             raise RuntimeError(f"one-shot all-gather setup failed on some rank (here: {err!r})")
         dist.barrier(group=group)   # every rank has mapped every buffer before the first launch
@@ -110,9 +116,7 @@ class OneShotAllGather:
 
     def failed_anywhere(self) -> bool:
         """failed() on ANY rank of the group (a collective: every rank must call it)."""
-        flag = torch.tensor([int(self.failed())], dtype=torch.int32, device=self.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-        return bool(flag.item())
+        return bool(_vote(self.failed(), dist.ReduceOp.MAX, self.group, self.device))
 
     def verify(self, sizes=(256, 2048, 14336), dtype=torch.float16) -> bool:
         """Compare with dist.all_gather_into_tensor on this group for a few payload sizes
@@ -133,9 +137,7 @@ class OneShotAllGather:
                         ok = ok and bool(torch.equal(a, b))
                     except Exception:  # noqa: BLE001 -- reported by the vote below
                         ok = False
-        flag = torch.tensor([int(ok and not self.failed())], device=self.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(flag.item())
+        return bool(_vote(ok and not self.failed(), dist.ReduceOp.MIN, self.group, self.device))
 
     def close(self) -> None:
         for p in self._opened:

@@ -139,6 +139,8 @@ def fuse_prenorm(model: nn.Module) -> int:
     (modeling_llama.py:306-321).  Call after fuse_projection_groups (and fuse_layer_ops);
     layers whose norm, groups or decoder forward do not match are left alone.  Returns the
     number of norms absorbed."""
+    from .parallel import RowShardedLinear4bit, sharded_group_compute
+
     n = 0
     for layer in model.modules():
         if type(layer).__name__ not in DECODER_CLASSES or "_qz_fused_decoder" in layer.__dict__:
@@ -153,9 +155,13 @@ def fuse_prenorm(model: nn.Module) -> int:
                 continue
             w = getattr(ln, "weight", None)
             members = [getattr(parent, nm, None) for nm in names]
-            g = members[0].__dict__.get("_qz_group") if isinstance(members[0], Linear4bit) else None
-            if w is None or not w.is_cuda or g is None or g.prenorm is not None or \
-                    g._compute is not _linear4bit_group_compute or \
+            g = members[0].__dict__.get("_qz_group") if isinstance(members[0], (Linear4bit, RowShardedLinear4bit)) \
+                else None
+            # Linear4bit groups, and groups of row shards (x is replicated: every rank normalises
+            # it in its own launch's prologue, the bits of the unsharded launch)
+            if w is None or g is None or g.prenorm is not None or \
+                    (g._compute is _linear4bit_group_compute and not w.is_cuda) or \
+                    g._compute not in (_linear4bit_group_compute, sharded_group_compute) or \
                     [id(m) for m in g.members] != [id(m) for m in members]:
                 continue
             g.prenorm = (w, float(ln.variance_epsilon), ln.forward)   # the norm as the model runs it now
@@ -233,6 +239,7 @@ def _fused_rope(orig):
 def _fused_mlp_forward(mod: nn.Module, pair: bool = True):
     from .layer_ops import silu_mul, silu_mul_supported
 
+    from . import parallel
     from .modules import linear4bit_silu_pair
 
     def forward(x: torch.Tensor, _qz_residual=None) -> torch.Tensor:
@@ -240,7 +247,10 @@ def _fused_mlp_forward(mod: nn.Module, pair: bool = True):
         grp = mod.gate_proj.__dict__.get("_qz_group")
         if pair and grp is not None and len(grp.members) == 2 and grp.members[0] is mod.gate_proj and \
                 grp.members[1] is mod.up_proj:
-            h = linear4bit_silu_pair(grp, x)   # gate, up and their product: one launch
+            # gate, up and their product: one launch (row shards: on this rank's rows, then one
+            # exchange of the product)
+            h = linear4bit_silu_pair(grp, x) if grp._compute is not parallel.sharded_group_compute \
+                else parallel.sharded_silu_pair(grp, x)
         if h is None:
             g = mod.gate_proj(x)  # same call order as LlamaMLP.forward (a DecodeGroup launches gate+up here)
             u = mod.up_proj(x)

@@ -111,12 +111,10 @@ class RowShardedLinear4bit(nn.Module):
             raise ValueError("prefill on a shard needs block-aligned second-level scales")
         return gemm_4bit(x, self.packed, self.state, bias=self.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        group = self.__dict__.get("_qz_group")
-        if group is not None and group.accepts(x):
-            return group.take(self, x)
-        y = self.local_forward(x)                       # [..., M/P]
-        if not self.gather:
+    def gather_rows(self, y: torch.Tensor) -> torch.Tensor:
+        """This rank's output rows [..., M/P] -> the full [..., M] on every rank (the
+        all-gather); column-parallel layers (gather=False) and world size 1 return y."""
+        if not self.gather or self.world_size == 1:
             return y
         lead = y.shape[:-1]
         rows = y.shape[-1]
@@ -129,6 +127,42 @@ class RowShardedLinear4bit(nn.Module):
         full = gathered.view(self.world_size, T, rows).permute(1, 0, 2).reshape(T, self.world_size * rows)
         return full.reshape(*lead, self.world_size * rows)
 
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        group = self.__dict__.get("_qz_group")
+        if group is not None and group.accepts(x):
+            return group.take(self, x)
+        if group is not None and group.prenorm is not None:
+            x = group.prenorm[2](x)      # prefill through a group that absorbed its RMSNorm
+        return self.gather_rows(self.local_forward(x))   # [..., M/P] -> [..., M]
+
+    def forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """residual + self(x), for LlamaDecoderLayer's residual adds (integration._project):
+        a single token's add rides in the local GEMV's epilogue on this rank's rows
+        (qz_gemv_4bit_residual: the same bits as the unsharded layer's fused epilogue), and the
+        rows are gathered afterwards.  Anything else: the two-op form."""
+        if (self._local_matmul is None and self.gather and x.is_cuda and x.numel() == x.shape[-1]
+                and residual.dtype == x.dtype and residual.is_contiguous() and residual.numel() == self.out_features
+                and self.__dict__.get("_qz_group") is None):
+            from .core import gemv_4bit
+            rows = residual.reshape(-1)[self.r0:self.r1]
+            y = gemv_4bit(x, self.packed, state=self.state, bias=self.bias, block_base=self.block_base,
+                          exact_codes=self.exact_codes, residual=rows)
+            return self.gather_rows(y).reshape(residual.shape)
+        return residual + self(x)
+
+
+def _group_input(group, x: torch.Tensor, fused_ok: bool):
+    """The input the members multiply and the norm for the launch: a DecodeGroup's absorbed
+    RMSNorm (integration.fuse_prenorm) rides inside a single-token launch where the kernel
+    takes it (fused_ok), else it runs first as the model ran it."""
+    norm = group.prenorm
+    if norm is None:
+        return x, None
+    if (fused_ok and x.is_cuda and x.numel() == x.shape[-1] and norm[0].dtype == x.dtype
+            and norm[0].is_contiguous() and norm[0].numel() == x.shape[-1]):
+        return x, norm[:2]
+    return norm[2](x), None
+
 
 def _sharded_group_tokens(group, x: torch.Tensor):
     """T = 2..16 decode tokens (a small batch of streams): ONE grouped
@@ -137,6 +171,7 @@ def _sharded_group_tokens(group, x: torch.Tensor):
     from .core import gemm_4bit_grouped, grouped_tokens_ok
 
     ms = group.members
+    x, _ = _group_input(group, x, fused_ok=False)
     K = x.shape[-1]
     T = x.numel() // K
     lead = x.shape[:-1]
@@ -147,7 +182,7 @@ def _sharded_group_tokens(group, x: torch.Tensor):
         outs = gemm_4bit_grouped(x, items)
     else:
         outs = [m.local_forward(x) for m in ms]
-    if not ms[0].gather:  # column-parallel: each member keeps its shard
+    if not ms[0].gather or ms[0].world_size == 1:  # column-parallel / one rank: nothing to exchange
         return [o.reshape(*lead, o.shape[-1]) for o in outs]
     rows = [m.r1 - m.r0 for m in ms]
     S = sum(rows)
@@ -174,6 +209,7 @@ def sharded_group_compute(group, x: torch.Tensor):
     if x.numel() != x.shape[-1]:
         return _sharded_group_tokens(group, x)
     ms = group.members
+    x, norm = _group_input(group, x, fused_ok=ms[0]._local_matmul is None)
     rows = [m.r1 - m.r0 for m in ms]
     S = sum(rows)
     buf = torch.empty(S, dtype=x.dtype, device=x.device)
@@ -186,9 +222,9 @@ def sharded_group_compute(group, x: torch.Tensor):
             v.copy_(m._local_matmul(x, m).reshape(-1))
     else:
         gemv_4bit_grouped(x, [(m.packed, m.state, m.bias, m.block_base, v) for m, v in zip(ms, views)],
-                          exact_codes=ms[0].exact_codes)
+                          exact_codes=ms[0].exact_codes, norm=norm)
     lead = x.shape[:-1]
-    if not ms[0].gather:  # column-parallel: each member keeps its shard
+    if not ms[0].gather or ms[0].world_size == 1:  # column-parallel / one rank: nothing to exchange
         return [v.view(*lead, r) for v, r in zip(views, rows)]
     P = ms[0].world_size
     gathered = torch.empty(P * S, dtype=x.dtype, device=x.device)
@@ -199,6 +235,33 @@ def sharded_group_compute(group, x: torch.Tensor):
         outs.append(g2[:, o:o + r].reshape(*lead, P * r))
         o += r
     return outs
+
+
+def sharded_silu_pair(group, x: torch.Tensor) -> Optional[torch.Tensor]:
+    """act_fn(gate_proj(x)) * up_proj(x) for a decode group of exactly the row shards of
+    (gate_proj, up_proj) and a single token: ONE launch on this rank's rows
+    (core.gemv_4bit_pair_silu with the shards' block_base, an absorbed RMSNorm inside), then
+    ONE all-gather of the [M/P] product h -- instead of the grouped launch, the exchange of
+    gate AND up, and a separate SiLU-product launch.  Column-parallel shards (the Megatron
+    pairing) keep their h rows: they are exactly what the row-parallel down_proj takes.  None
+    when the launch does not take the case (the caller then calls the members)."""
+    ms = group.members
+    if group._compute is not sharded_group_compute or len(ms) != 2 or x.numel() != x.shape[-1]:
+        return None
+    g, u = ms
+    if (g.r0, g.r1) != (u.r0, u.r1) or g.exact_codes != u.exact_codes or \
+            (g._local_matmul is None and not (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16))):
+        return None
+    xin, norm = _group_input(group, x, fused_ok=g._local_matmul is None)
+    if g._local_matmul is not None:  # test hook (CPU): the two local products and torch's SiLU
+        h = torch.nn.functional.silu(g._local_matmul(xin, g)) * u._local_matmul(xin, u)
+    else:
+        from .core import gemv_4bit_pair_silu
+        h = gemv_4bit_pair_silu(xin, [(g.packed, g.state, g.bias, g.block_base), (u.packed, u.state, u.bias, u.block_base)],
+                                exact_codes=g.exact_codes, norm=norm)
+        if h is None:
+            return None
+    return g.gather_rows(h.reshape(*x.shape[:-1], g.r1 - g.r0))
 
 
 def consumer_absmax(qs: QuantState) -> torch.Tensor:

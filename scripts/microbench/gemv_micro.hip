@@ -385,6 +385,69 @@ int main(int argc, char **argv) {
     GVWN(2, 4, false, false); GVWN(2, 4, true, false); GVWN(2, 8, true, true); GVWN(2, 8, true, false);
     GVWN(1, 8, true, true);
   }
+  // outputs of every registered variant from the first whose name holds `ref` on, against it
+  auto check_outputs = [&](const char *ref) {
+      std::vector<uint16_t> hx(K);
+      uint32_t st = 12345u;
+      for (int k = 0; k < K; ++k) {
+        st = st * 1664525u + 1013904223u;
+        hx[k] = (uint16_t)(0x3000u + ((st >> 8) & 0x0FFFu)) | ((st >> 30) << 15);
+      }
+      CK(hipMemcpy(x, hx.data(), K * 2, hipMemcpyHostToDevice));
+      std::vector<std::vector<uint16_t>> outs;
+      size_t v0 = 0;
+      while (v0 < vs.size() && vs[v0].name.find(ref) == std::string::npos) ++v0;
+      for (size_t vi = v0; vi < vs.size(); ++vi) {
+        CK(hipMemset(y, 0, M * 4));
+        vs[vi].launch(0);
+        CK(hipDeviceSynchronize());
+        std::vector<uint16_t> hy(M);
+        CK(hipMemcpy(hy.data(), y, M * 2, hipMemcpyDeviceToHost));
+        outs.push_back(hy);
+      }
+      for (size_t o = 1; o < outs.size(); ++o) {
+        int diff = 0, maxulp = 0;
+        for (int r = 0; r < M; ++r) {
+          const int d = std::abs((int)(int16_t)outs[o][r] - (int)(int16_t)outs[0][r]);
+          if (d) ++diff;
+          maxulp = std::max(maxulp, d);
+        }
+        printf("check %-40s vs product CL: %d of %d fp16 outputs differ, max %d ulp\n", vs[v0 + o].name.c_str(), diff, M,
+               maxulp);
+      }
+      CK(hipMemset(x, 0x3C, (size_t)K * 4 * 64));
+  };
+  const bool fm = argc > 4 && std::string(argv[4]) == "fm";
+  // exact codes (CL): FMV 0 = hi + lo fp16 code pairs by v_dot2c (round-3 product); 1 = fp32 codes
+  // by v_fma_mix_f32, two-VALU addresses, 16-copy table; 2 = the same, 256-B entries + SDWA addresses
+#define GVM(R, NW, WT_, FMV_) timeit("gemvFS CL R=" #R " NW=" #NW " WT=" #WT_ " FMV=" #FMV_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.out_scale = (FMV_) ? 1.0f : 1.0f / 16384; q.tabsel = 0; \
+    const unsigned g = (unsigned)((M + R * NW - 1) / (R * NW)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, NW, false, 0, true, true, WT_, FMV_>), dim3(g), dim3(NW * 64), 0, 0, q); })
+  if (fm) {
+    GVFS(2, 0);                                      // fp16 codes (reference point)
+    GVM(2, 4, false, 0); GVM(2, 4, false, 1); GVM(2, 4, true, 1); GVM(2, 4, true, 2);
+    GVM(4, 4, false, 0); GVM(4, 4, false, 1); GVM(4, 4, true, 2);
+    GVM(1, 4, false, 1); GVM(1, 4, true, 2);
+    GVM(2, 8, true, 2); GVM(4, 8, true, 2); GVM(1, 8, true, 2);
+    check_outputs("FMV=0");
+  }
+  const bool early = argc > 4 && std::string(argv[4]) == "early";
+  // OPT 1: the second K-step issued before the prologue barrier; 2: byte table built from SGPR planes
+#define GVO(R, CL_, OPT_) timeit("gemvFS R=" #R " CL=" #CL_ " OPT=" #OPT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.tabsel = (CL_) ? 2 : 0; \
+    if (CL_) { q.out_scale = 1.0f / 16384; build_exact_planes(q.tab, q.tab_lo); } \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, CL_, false, 0, OPT_>), dim3(g), dim3(256), 0, 0, q); })
+  if (early) {
+    GVO(2, true, 0); GVO(2, true, 1); GVO(2, true, 2); GVO(2, true, 3);
+    GVO(2, false, 0); GVO(2, false, 1); GVO(2, false, 3);
+    GVO(4, true, 0); GVO(4, true, 1); GVO(4, true, 3);
+    GVO(1, true, 0); GVO(1, true, 3);
+    check_outputs("R=2 CL=true OPT=0");
+  }
   const bool stream = argc > 4 && std::string(argv[4]) == "stream";
 #define GVST(R, G, CL_) timeit("stream2 R=" #R " wgs=" #G " CL=" #CL_, [&, pt = p](int i) { \
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
@@ -398,7 +461,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
@@ -475,6 +538,13 @@ int main(int argc, char **argv) {
       run("gemv tab DQ R=2 full-step exact codes (product)", g * 4, [&, pt = p](int i) {
         GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
         hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true>), dim3(g), dim3(256), 0, 0, q); });
+      run("gemv tab DQ R=2 full-step exact codes, second step before the barrier (OPT 1)", g * 4, [&, pt = p](int i) {
+        GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
+        hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true, false, 0, 1>), dim3(g), dim3(256), 0, 0, q); });
+      run("gemv tab DQ R=2 full-step exact codes, SGPR table (OPT 2)", g * 4, [&, pt = p](int i) {
+        GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
+        build_exact_planes(q.tab, q.tab_lo);
+        hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true, false, 0, 2>), dim3(g), dim3(256), 0, 0, q); });
     }
     return 0;
   }

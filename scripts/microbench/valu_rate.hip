@@ -26,6 +26,9 @@ __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, int n, uint32_t se
       else if constexpr (OP == 4) f[i] = __builtin_fmaf(f[i], 1.0001f, 0.5f);
       else if constexpr (OP == 5) a[i] = a[i] ^ b;
       else if constexpr (OP == 6) { h2 r = __builtin_bit_cast(h2, a[i]) * __builtin_bit_cast(h2, b) + __builtin_bit_cast(h2, c); a[i] = __builtin_bit_cast(uint32_t, r); }
+      else if constexpr (OP == 7) asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(f[i]) : "v"(b), "v"(c));
+      else if constexpr (OP == 8) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a[i]) : "v"(b));
+      else if constexpr (OP == 9) asm volatile("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(a[i]) : "v"(a[i]), "v"(c));
     }
   }
   unsigned long long t1 = __builtin_readcyclecounter();
@@ -40,10 +43,10 @@ int main() {
   uint32_t *out; unsigned long long *cyc;
   CK(hipMalloc(&out, 256 * 1024 * 4 * 8)); CK(hipMalloc(&cyc, 8));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  const char *names[] = {"v_perm_b32", "v_bfi_b32", "lshr+and (2 ops)", "v_dot2c_f32_f16", "v_fma_f32", "v_xor_b32", "v_pk_fma_f16"};
+  const char *names[] = {"v_perm_b32", "v_bfi_b32", "lshr+and (2 ops)", "v_dot2c_f32_f16", "v_fma_f32", "v_xor_b32", "v_pk_fma_f16", "v_fma_mix_f32", "v_mov_b32_sdwa", "v_lshl_or_b32"};
   const int n = 4096;
   for (int wps : {1, 2, 4, 8}) {
-    for (int op = 0; op < 7; ++op) {
+    for (int op = 0; op < 10; ++op) {
       const int threads = 256 * wps;  // one block per CU: 4 SIMDs x wps waves
       auto launch = [&]() {
         switch (op) {
@@ -54,6 +57,9 @@ int main() {
           case 4: hipLaunchKernelGGL(k_rate<4>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
           case 5: hipLaunchKernelGGL(k_rate<5>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
           case 6: hipLaunchKernelGGL(k_rate<6>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
+          case 7: hipLaunchKernelGGL(k_rate<7>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
+          case 8: hipLaunchKernelGGL(k_rate<8>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
+          case 9: hipLaunchKernelGGL(k_rate<9>, dim3(256), dim3(threads), 0, 0, out, n, 1u, cyc); break;
         }
       };
       launch(); CK(hipDeviceSynchronize());

@@ -304,7 +304,7 @@ def test_tensor_parallel_pairing_tiny_llama(batch, oneshot):
         assert rel < 1e-5 and rel_step < 1e-5, (rank, rel, rel_step)
 
 
-def _bench_layout_worker(rank, world, port, q, tp_mode, batch):
+def _bench_layout_worker(rank, world, port, q, tp_mode, batch, layer_ops="none"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -312,12 +312,38 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch):
         from quantizations_amd.parallel import RowShardedLinear4bit
 
         cfg, model, ref = _tiny_llama_4bit()
-        n_groups, _ = bench.prepare_decode_model(model, rank, world, True, tp_mode, fuse=True, layer_ops="none",
-                                                 local_matmul=_tp_hook)
+        n_groups, n_ops = bench.prepare_decode_model(model, rank, world, True, tp_mode, fuse=True,
+                                                     layer_ops=layer_ops, local_matmul=_tp_hook)
+        if layer_ops != "none":
+            # the fused decoder layer on row shards: both norms absorbed into the sharded groups, the
+            # MLP's gate/up + SiLU product as one local launch + one exchange of h, the residual adds
+            # handed to o_proj / down_proj (forward_residual)
+            from quantizations_amd.parallel import RowShardedLinear4bit
+            lay = model.model.layers[0]
+            grp = lay.mlp.gate_proj.__dict__["_qz_group"]
+            assert grp.prenorm is not None and lay.self_attn.q_proj.__dict__["_qz_group"].prenorm is not None
+            assert "_qz_residual_decoder" in lay.__dict__
+            calls = {"pair": 0, "res": 0}
+            import quantizations_amd.parallel as par
+            orig_pair, orig_res = par.sharded_silu_pair, RowShardedLinear4bit.forward_residual
+
+            def pair_spy(g, x):
+                calls["pair"] += 1
+                return orig_pair(g, x)
+
+            def res_spy(self, x, r):
+                calls["res"] += 1
+                return orig_res(self, x, r)
+            par.sharded_silu_pair = pair_spy
+            RowShardedLinear4bit.forward_residual = res_spy
         # bench.py's own decode loop (StaticCache, static token/position buffers, token
         # feedback), eagerly on CPU; the reference is the unsharded dequantised model
         _, hist = bench.decode_bench_graph(model, cfg, steps=5, warmup=2, prompt_len=6, world=world, batch=batch,
                                            graph=False, device="cpu")
+        if layer_ops != "none":
+            par.sharded_silu_pair, RowShardedLinear4bit.forward_residual = orig_pair, orig_res
+            assert calls["res"] > 0 or tp_mode == "pair", calls
+            assert (calls["pair"] > 0) == (batch == 1), calls
         _, ref_hist = bench.decode_bench_graph(ref, cfg, steps=5, warmup=2, prompt_len=6, world=1, batch=batch,
                                                graph=False, device="cpu")
         q_proj = model.model.layers[0].self_attn.q_proj
@@ -327,20 +353,23 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("tp_mode,batch", [("gather", 1), ("pair", 2)])
-def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch):
+@pytest.mark.parametrize("tp_mode,batch,layer_ops", [("gather", 1, "none"), ("pair", 2, "none"), ("gather", 1, "all"),
+                                                    ("pair", 1, "all")])
+def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops):
     """bench.py --gpus 2 exactly as the driver runs it, on gloo world 2 with the
     oracle as each shard's local product: the default strong-scaling layout
     (one bs=1 stream, every Linear4bit row-split + all-gather) and the
     weak-scaling extra (two streams, Megatron pairing).  The greedy tokens of 7
-    decode steps equal the unsharded model's on every rank."""
+    decode steps equal the unsharded model's on every rank.  layer_ops "all": the
+    fused decoder layer on the shards (absorbed norms, the sharded SiLU pair, the
+    residual epilogues), as bench.py sets it up for N > 1."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     os.environ["PYTHONPATH"] = REPO + os.pathsep + os.path.join(REPO, "tests") + os.pathsep + \
         os.environ.get("PYTHONPATH", "")
-    procs = [ctx.Process(target=_bench_layout_worker, args=(r, world, port, q, tp_mode, batch))
+    procs = [ctx.Process(target=_bench_layout_worker, args=(r, world, port, q, tp_mode, batch, layer_ops))
              for r in range(world)]
     for p in procs:
         p.start()

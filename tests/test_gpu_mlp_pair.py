@@ -57,6 +57,31 @@ def test_pair_silu_fp4_without_double_quant():
     assert torch.equal(gemv_4bit_pair_silu(x, items), F.silu(gate) * up)
 
 
+@pytest.mark.parametrize("world,rank", [(8, 3), (2, 1), (4, 0)])
+def test_pair_silu_on_row_shards(world, rank):
+    """The pair launch on row shards of gate/up (parallel.sharded_silu_pair's local launch:
+    block_base addressing; at 8 ranks the geometry is one row per wave, R = 1): bit-identical
+    to the grouped launch + product on the same shards AND to the unsharded pair's rows."""
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
+    from quantizations_amd.parallel import shard_rows
+
+    M, K = 14336, 4096
+    items = _items(M, K, torch.float16, seed=21)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).half()
+    nw = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).half()
+    full = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=(nw, 1e-5))
+    shards = [shard_rows(p, st, rank, world) for p, st, _ in items]
+    sh_items = [(sh.packed, sh.state, None, sh.block_base) for sh in shards]
+    h = gemv_4bit_pair_silu(x, sh_items, exact_codes=True, norm=(nw, 1e-5))
+    gate, up = gemv_4bit_grouped(x, sh_items, exact_codes=True, norm=(nw, 1e-5))
+    torch.cuda.synchronize()
+    r0, r1 = shards[0].r0, shards[0].r1
+    assert h is not None and h.shape[-1] == r1 - r0
+    assert torch.equal(h, F.silu(gate) * up)
+    assert torch.equal(h.reshape(-1), full.reshape(-1)[r0:r1])
+
+
 def test_pair_silu_declines_what_it_cannot_take():
     """Geometries that split rows over waves (K = 8192; small pairs), odd K, fp32 x, unequal
     shapes: None, nothing launched (the grouped launch + product then run)."""

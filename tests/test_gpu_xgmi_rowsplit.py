@@ -58,12 +58,23 @@ def _work(rank, world, port, q, layout):
         cfg, model = _model(dev)
         ref = copy.deepcopy(model)
         ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
-        if layout == "gather":
+        if layout.startswith("gather"):
             shard_model_linear4bit(model, rank, world, gatherer=ag)
         else:   # Megatron pairing: column q/k/v/gate/up, row o/down with the one-shot all-reduce
             apply_tensor_parallel(model, rank, world, gatherer=ag)
         n_groups = fuse_projection_groups(model)
         fuse_projection_groups(ref)
+        if layout.endswith("fused"):
+            # the fused decoder layer on the shards, as bench.py runs N > 1: both RMSNorms inside the
+            # sharded q/k/v and gate/up launches, gate/up + SiLU as one launch on the local rows, the
+            # residual adds in the o/down epilogues, the one-launch decode attention
+            from quantizations_amd.integration import fuse_layer_ops, fuse_prenorm
+            for m in (model, ref):
+                fuse_layer_ops(m)
+                assert fuse_prenorm(m) == 2 * cfg.num_hidden_layers
+        lay = model.model.layers[0]
+        fused_ok = (not layout.endswith("fused")) or (
+            lay.mlp.gate_proj.__dict__["_qz_group"].prenorm is not None and "_qz_residual_decoder" in lay.__dict__)
         ids = torch.randint(0, cfg.vocab_size, (1, 12), generator=torch.Generator().manual_seed(5)).to(dev)
         with torch.inference_mode():
             a = model(input_ids=ids).logits.float()          # prefill: multi-token shard launches
@@ -81,15 +92,15 @@ def _work(rank, world, port, q, layout):
         dist.all_gather_object(allh, hist)
         q0 = model.model.layers[0].self_attn.q_proj
         q.put((rank, n_groups, prefill_rel, decode_rel, bool(torch.equal(allh[0], allh[1])),
-               int((hist[:, 8:16] != 0).sum()), ag.failed(), isinstance(q0, RowShardedLinear4bit),
-               q0.r1 - q0.r0, q0.r0))
+               int((hist[:, 8:16] != 0).sum()), ag.failed_anywhere(), isinstance(q0, RowShardedLinear4bit),
+               q0.r1 - q0.r0, q0.r0, fused_ok))
         dist.barrier()
         ag.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["gather", "pair"])
+@pytest.mark.parametrize("layout", ["gather", "pair", "gather-fused", "pair-fused"])
 def test_rowsplit_world2_oneshot_on_gpu(layout):
     world = 2
     ctx = mp.get_context("spawn")
@@ -111,8 +122,9 @@ def test_rowsplit_world2_oneshot_on_gpu(layout):
         assert r[1] != "error", f"rank {r[0]}: {r[2]}"
     for p in procs:
         assert p.exitcode == 0
-    for rank, n_groups, prefill_rel, decode_rel, same, n_tok, failed, sharded, rows, r0 in res:
+    for rank, n_groups, prefill_rel, decode_rel, same, n_tok, failed, sharded, rows, r0, fused_ok in res:
         assert sharded and rows == 256 and n_groups == 4, (rank, rows, n_groups)
+        assert fused_ok, "the fused layer was not installed on the shards"
         assert r0 == 256 * rank                      # q_proj rows [256 rank, +256) of 512
         assert not failed, f"rank {rank}: an exchange timed out"
         # row shards multiply the global state's exact weights; fp32 summation order and the

@@ -531,9 +531,98 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "other_codes_launch_us": round(other_us, 3), "plain_grouped_launch_us": round(plain_us, 3),
-            "traffic": _pmc_traffic("r3_gateup_pmc.json"),
-            "profile": "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the "
-                       "launch without the norm)"}
+            "traffic": _pmc_traffic("r4_pair_pmc.json") if (prenorm and pair) else _pmc_traffic("r3_gateup_pmc.json"),
+            "profile": ("profiles/r4_pair_pmc.json (rocprofv3 FETCH/WRITE passes of THIS launch: the pair with the "
+                        "norm and SiLU, exact codes; SQ counters profiles/r4_pair_prenorm_sq_counters.txt)"
+                        if (prenorm and pair) else
+                        "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the grouped "
+                        "launch without the norm)")}
+
+
+@torch.inference_mode()
+def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10):
+    """The Linear4bit chain of a Llama-3-8B decoder layer as the bench decode runs it -- q/k/v
+    (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
+    paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
+    `copies` rotating weight sets (8 x 113 MB > the 256 MiB Infinity Cache) captured in ONE HIP
+    graph: algorithmic bytes / time for the chain, i.e. the single-launch roofline with the
+    dependent-launch gaps of a real decode step included (the attention launch between q/k/v and
+    o_proj is left out: it is not a Linear4bit; o_proj reads the q output in its place, so every
+    launch still depends on the previous one)."""
+    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
+
+    dev = torch.device("cuda")
+    torch.manual_seed(11)
+    base = {}
+    for name, (M, K) in zip(("q", "k", "v", "o", "gate", "up", "down"), LAYER_SHAPES):
+        W = (torch.randn(M, K, device=dev) * 0.02).to(torch.float16)
+        base[name] = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
+        del W
+
+    def clone(pk, qs):
+        st = type(qs)(absmax=qs.absmax.clone(), shape=qs.shape, code=qs.code, blocksize=qs.blocksize,
+                      quant_type=qs.quant_type, dtype=qs.dtype, offset=qs.offset.clone(),
+                      state2=type(qs.state2)(absmax=qs.state2.absmax.clone(), code=qs.state2.code,
+                                             blocksize=qs.state2.blocksize, dtype=qs.state2.dtype))
+        return pk.clone(), st
+    sets = [{n: clone(*base[n]) for n in base} for _ in range(copies)]
+    del base
+    H, I = 4096, 14336
+    nw1 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
+    nw2 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
+    x0 = torch.randn(1, 1, H, device=dev).half()
+    qkv_out = [torch.empty(H, device=dev, dtype=torch.float16), torch.empty(1024, device=dev, dtype=torch.float16),
+               torch.empty(1024, device=dev, dtype=torch.float16)]
+
+    def layer(x, w):
+        q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
+                                        (*w["v"], None, 0, qkv_out[2])], exact_codes=True, norm=(nw1, 1e-5))
+        a = gemv_4bit(q.view(1, 1, H), w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1))
+        h = gemv_4bit_pair_silu(a, [(*w["gate"], None), (*w["up"], None)], exact_codes=True, norm=(nw2, 1e-5))
+        assert h is not None
+        return gemv_4bit(h, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1))
+
+    def chain():
+        x = x0
+        for i in range(layers):
+            x = layer(x, sets[i % copies])
+        return x
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        chain()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        chain()
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    times = []
+    for _ in range(reps):
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e3 / layers)
+    us = statistics.median(times)
+    # algorithmic bytes per layer: the four launches' GEMV bytes (SURVEY 8d), + the two norm
+    # weights and the two residual reads, - the pair's second output (it writes h only)
+    nbytes = (gemv_alg_bytes([(H, H), (1024, H), (1024, H)]) - 2 * (2 * H)   # q/k/v: x read once, not 3 x
+              + gemv_alg_bytes([(H, H)]) + 2 * H                                # o_proj + its residual read
+              + gemv_alg_bytes([(I, H)] * 2) - 2 * H - 2 * I                    # pair: x once, one [I] output
+              + gemv_alg_bytes([(H, I)]) + 2 * H                                # down_proj + its residual read
+              + 2 * (2 * H))                                                    # the two RMSNorm weights
+    del sets, g
+    torch.cuda.empty_cache()
+    ach = nbytes / (us * 1e-6) / 1e9
+    return {"what": "one Llama-3-8B layer's Linear4bit chain: q/k/v+norm grouped, o_proj+residual, gate/up+SiLU+norm "
+                    "pair, down_proj+residual (4 dependent launches), NF4+DQ exact codes, one HIP graph of "
+                    f"{layers} layers over {copies} rotating weight sets",
+            "us_per_layer": round(us, 3), "us_per_launch": round(us / 4, 3), "algorithmic_bytes_per_layer": nbytes,
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "us_per_layer_min": round(min(times), 3), "us_per_layer_max": round(max(times), 3)}
 
 
 def _pmc_traffic(name: str):
@@ -892,6 +981,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--gemv-only", action="store_true", help="only the 4096x4096 roofline microbench (profiling)")
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
+    ap.add_argument("--chain-only", action="store_true",
+                    help="only the Linear4bit chain of one decoder layer (chain_roofline; profiling)")
     ap.add_argument("--dominant-only", action="store_true",
                     help="only the grouped gate/up GEMV measurement (the decode step's longest launch; profiling)")
     ap.add_argument("--no-prefill", action="store_true")
@@ -986,6 +1077,9 @@ def main():
     if args.dominant_only:
         print(json.dumps(dominant_roofline()), flush=True)
         return
+    if args.chain_only:
+        print(json.dumps(chain_roofline()), flush=True)
+        return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
         return
@@ -1062,6 +1156,7 @@ def main():
 
     roof = None
     parity = None
+    chain = None
     if rank == 0 and not args.no_roofline:
         mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
         # average launch duration = HIP events around `iters` back-to-back launches on
@@ -1098,6 +1193,7 @@ def main():
             roof["in_kernel_us"] = ink["in_kernel_us"]
             roof["frac_in_kernel"] = round(GEMV_BYTES_4096 / (ink["in_kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         parity = gemv_parity()
+        chain = chain_roofline()
 
     layer = None
     if not args.no_roofline:
@@ -1155,6 +1251,8 @@ def main():
             line["config"]["exchange"] = exchange
         if extra_codes is not None:
             line["decode_other_codes"] = extra_codes
+        if chain is not None:
+            line["chain_roofline"] = chain
         if layer is not None:
             line["rowsplit_layer"] = layer
         if extra_weak is not None:

@@ -229,6 +229,11 @@ struct GemvParams {
   const void *nw;    // fused pre-norm (NRM): the RMSNorm weight [K], or nullptr
   float eps;         //   and its epsilon
   const void *res;   // residual [M] added after the output rounding (y = round(round(x W^T) + res)), or nullptr
+  // prefetch (PF): the first pf_chunks KiB of each of pf_rows rows (stride pf_row_bytes) of the NEXT
+  // launch's packed weight, read into the caches (Infinity Cache) once this launch's own loads are out
+  const unsigned char *pf;
+  uint32_t pf_row_bytes;
+  int pf_rows, pf_chunks;
 };
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -325,6 +330,10 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   for (int i = 0; i < 8; ++i) p.tab_lo[i] = keep_s(in.tab_lo[i]);
   p.nw = keep_sp(in.nw);
   p.eps = keep_s(in.eps);
+  p.pf = keep_sp(in.pf);
+  p.pf_row_bytes = keep_s(in.pf_row_bytes);
+  p.pf_rows = keep_s(in.pf_rows);
+  p.pf_chunks = keep_s(in.pf_chunks);
   return p;
 }
 
@@ -881,7 +890,8 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0>
+          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0,
+          bool PF = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
                                           const GemvParams *pair = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
@@ -1159,6 +1169,23 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // register whose load is in flight forces vmcnt(0) -- the prefetch is then
   // waited for before the current step is decoded.  Every consume(cur) below
   // reads the same registers on every path, so no copies are needed.
+  // PF: this wave's share of the next launch's first K-steps, issued after its own last loads (so no
+  // wait for its own data waits for them); the values are discarded after the stores
+  constexpr int kPfMax = PF ? 4 : 1;
+  uint32_t pfv[kPfMax];
+  auto prefetch = [&]() {
+    if constexpr (PF) {
+      const int W = (int)gridDim.x * NW, gw = block * NW + wave;
+      const int items = p.pf_rows * p.pf_chunks;
+#pragma unroll
+      for (int i = 0; i < kPfMax; ++i) {
+        const int it = min(gw + i * W, items - 1);
+        const int r = it / p.pf_chunks, ck = it - r * p.pf_chunks;
+        const uint32_t off = (uint32_t)r * p.pf_row_bytes + ((uint32_t)ck << 10) + ((uint32_t)lane << 4);
+        pfv[i] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p.pf + off));
+      }
+    }
+  };
   if (kEarly && have) {
     // `other` already holds step s + WK (n >= 2); at the loop top cur = step j, other = j + 1
     const int n = n_my;
@@ -1199,11 +1226,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     if (n - j == 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
+      prefetch();
       __builtin_amdgcn_sched_barrier(0);
       consume(cur);
       QZ_STAMP(2);
       consume(other);
     } else {
+      prefetch();
       consume(cur);
     }
   }
@@ -1278,6 +1307,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     QZ_STAMP(4);
     QZ_STAMP_FLUSH(block * NW + wave);
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < kPfMax; ++i) asm volatile("" ::"v"(pfv[i]));
+    }
     return;
   }
 #pragma unroll
@@ -1301,9 +1334,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0>
+          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0, bool PF = false>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT, PF>(p, blockIdx.x);
 }
 
 // Streaming ("persistent") form for rows of exactly NS K-steps (K = 2048 * NS, full-step
@@ -1412,6 +1445,276 @@ __device__ __forceinline__ void gemv_stream2_body(const GemvParams &p_in, int nu
 template <bool DQ, int R, bool CL, int ABL = 0>
 __global__ __launch_bounds__(256) void k_gemv_4bit_stream2(GemvParams p, int nunits) {
   gemv_stream2_body<DQ, R, CL, ABL>(p, nunits);
+}
+
+// ---------------------------------------------------------------------------
+// MFMA-product decode GEMV (round 4, experimental: k_gemv_4bit_mf).  The byte table's
+// entries ARE v_mfma_f32_16x16x32_f16 operand fragments: a lane's 16 packed bytes decode
+// through the table into 32 codes = four 8-code fragments with no VALU after the LDS read,
+// so the matrix pipe takes the products and the VALU keeps only the table addresses.
+//  * a wave owns a 16-row tile: lane l reads row (l & 15), 16-B chunk g = l >> 4 of each 64-B
+//    row segment; one load instruction covers 16 rows x 128 elements (1 KiB);
+//  * the codes are the B operand (lane l supplies B[k = 8 g + jj][n = l & 15]: weight row n,
+//    codes 8j..8j+7 of chunk g for MFMA j) and x is a "diagonal" A operand: A[m][8 g + jj] =
+//    x of chunk g if m == g, else 0 -- the lanes with (l & 15) == (l >> 4) load x, the others
+//    load zeros (a zero buffer, so no select and no exec mask);
+//  * so C[m = g][n = row] is chunk g's unscaled dot of that row, which the 16x16 C layout puts
+//    in lane `row` (0..15), register g: each of lanes 0..15 scales its row's four chunks by
+//    their blocks' absmax and keeps ONE running sum -- no cross-lane reduction;
+//  * exact codes add the lo fragments into the same C (hi + lo = the fp32 code to ~2^-23);
+//  * NWK waves split K; the per-row partials meet in LDS.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+__device__ const uint32_t g_mf_zeros[512] = {};   // the inactive lanes' A fragments (2 KiB of zeros)
+
+template <bool CL, bool WT, int NWK, int NL>
+__global__ __launch_bounds__(NWK * 64) void k_gemv_4bit_mf(GemvParams p_in) {
+  const GemvParams p = load_params(p_in);
+  constexpr int kPieces = WT ? 16 : kTabCopies / 4;
+  static_assert(NL % 2 == 0 && NL <= 8, "2 NL qabsmax bytes per row come as whole dwords");
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[(WT ? 2 : 1) * kTabDwords];
+  __shared__ float s_code2[256];
+  __shared__ float s_part[NWK][16];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int row0 = blockIdx.x * 16;
+  const int rl = lane & 15, g = lane >> 4;           // this lane's row in the tile, its 16-B chunk
+  const uint32_t row_bytes = (uint32_t)p.K >> 1;
+  // 1. code2 and the table entry (the barrier waits for them), then every weight load
+  float c2 = 0.0f;
+  if (threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x];
+  const float offset = *p.sc.offset;
+  u32x4 tab_entry = {0u, 0u, 0u, 0u};
+  if (threadIdx.x < 256) tab_entry = reinterpret_cast<const u32x4 *>((CL ? &g_byte_tab_nf4x : &g_byte_tab_nf4)->v)[threadIdx.x];
+  const uint32_t kb0 = (uint32_t)(wave * NL) * 64u;  // this wave's first byte within a row
+  const unsigned char *rowp = p.B + (size_t)(uint32_t)(row0 + rl) * row_bytes;
+  u32x4 wv[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+    wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + kb0 + 64u * i + 16u * g));
+  // x: A fragment (i, j) = 16 B at 4 kb0 + 64 g + 256 i + 16 j in the diagonal lanes, zeros elsewhere
+  typedef const __attribute__((address_space(1))) char *gcp;   // global, not flat, loads
+  u32x4 xa[NL][4];
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xa[i][j] = u32x4{0u, 0u, 0u, 0u};
+  if (rl == g) {   // four lanes load x (exec-masked: a quarter KiB per load, not a KiB of zeros)
+    const gcp xbase = (gcp)p.x + 4u * kb0 + 64u * (uint32_t)g;
+#pragma unroll
+    for (int i = 0; i < NL; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        xa[i][j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(xbase + 256 * i + 16 * j);
+  }
+  // scales of row (row0 + rl): its 2 NL blocks of this wave's range as NL / 2 dwords of qabsmax
+  const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;
+  const uint32_t b0 = (uint32_t)p.block_base + (uint32_t)(row0 + rl) * bpr + ((2u * kb0) >> p.bs_log2);
+  uint32_t qv[NL / 2];
+#pragma unroll
+  for (int t = 0; t < NL / 2; ++t) qv[t] = reinterpret_cast<const uint32_t *>(p.sc.qabsmax + b0)[t];
+  const float a2 = p.sc.absmax2[b0 >> p.bs2_log2];    // the 2 NL blocks share one (host-checked)
+  if (threadIdx.x < 256) {
+    s_code2[threadIdx.x] = c2;
+    store_byte_table_entry<kPieces>(s_tab, tab_entry);
+  }
+  __syncthreads();
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  const uint32_t jb = WT ? (uint32_t)(lane & 31) << 3 : (uint32_t)(lane & 15) << 3;
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const uint32_t w[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
+    uint32_t hi[16], lo[16];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        uint32_t a;
+        if constexpr (WT) a = __builtin_amdgcn_perm(w[d], jb, 0x0C0C0000u | ((4u + m) << 8));
+        else a = ((m == 0 ? (w[d] << 7) : (w[d] >> (8 * m - 7))) & 0x7F80u) | jb;
+        if constexpr (CL) {
+          const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a);
+          hi[4 * d + m] = e.x;
+          lo[4 * d + m] = e.y;
+        } else {
+          hi[4 * d + m] = *reinterpret_cast<const uint32_t *>(tb + a);
+        }
+      }
+    }
+    float4_t c = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const half8_t af = __builtin_bit_cast(half8_t, xa[i][j]);
+      const u32x4 bh = {hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, __builtin_bit_cast(half8_t, bh), c, 0, 0, 0);
+      if constexpr (CL) {
+        const u32x4 bl = {lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, __builtin_bit_cast(half8_t, bl), c, 0, 0, 0);
+      }
+    }
+    // chunks 0, 1 of load i lie in block 2 i, chunks 2, 3 in block 2 i + 1 (bytes of qv)
+    const uint32_t qw = qv[i >> 1];
+    const float am0 = __fadd_rn(__fmul_rn(s_code2[(qw >> (16 * (i & 1))) & 0xFFu], a2), offset);
+    const float am1 = __fadd_rn(__fmul_rn(s_code2[(qw >> (16 * (i & 1) + 8)) & 0xFFu], a2), offset);
+    acc = fmaf(__fadd_rn(c[0], c[1]), am0, acc);
+    acc = fmaf(__fadd_rn(c[2], c[3]), am1, acc);
+  }
+  if (lane < 16) s_part[wave][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < NWK; ++w) v += s_part[w][threadIdx.x];
+    const int row = row0 + (int)threadIdx.x;
+    float o = v * p.out_scale;
+    if (p.bias) o += load_f32<QZ_DT_F16>(p.bias, row);
+    store_f32<QZ_DT_F16>(p.y, row, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA-diagonal decode GEMV (round 4, experimental: k_gemv_4bit_dg).  The product GEMV's memory
+// layout -- a wave reads ONE row per load instruction, contiguously -- with the products on
+// the matrix pipe:
+//  * a segment is 1024 elements (512 B) of a row; lane l owns its 16-element chunk
+//    c(l) = 4 (l & 15) + (l >> 4), i.e. 8 B at 8 c(l): one dwordx2 per lane per segment;
+//  * v_mfma_f32_16x16x32_f16 with the lane's codes as A (A[m = l & 15][k = 8 (l >> 4) + jj])
+//    and the lane's OWN x as B (B[k = 8 (l >> 4) + jj][n = l & 15]): C[m][n] sums the four k
+//    groups g of lanes m + 16 g (codes) against lanes n + 16 g (x), so the diagonal m == n is
+//    sum_g codes(chunk 4 m + g) . x(chunk 4 m + g) = the dot of scale block m of the segment
+//    (chunks 4m..4m+3 = elements 64m..64m+63): one absmax per diagonal element;
+//  * exact codes: an A fragment is two table entries as they land from two ds_read_b64,
+//    {hi pair, lo pair} of bytes 2f and 2f + 1 = codes (ch, ch, cl, cl, ch, ch, cl, cl), and B
+//    the matching x pairs doubled (x, x, x, x of 4f..4f+3 as (x0 x1 x0 x1 x2 x3 x2 x3)) -- built
+//    once per segment and shared by the R rows;
+//  * the diagonal C[m][m] sits in lane m + 16 (m >> 2), register m & 3: every lane scales its
+//    four C registers by its block's absmax into four running sums per row and keeps the one
+//    with index m & 3 at the end; 16 lanes x NWK waves meet in LDS.
+// ---------------------------------------------------------------------------
+template <bool CL, int R, int NSEG, int NWK>
+__global__ __launch_bounds__(NWK * 64) void k_gemv_4bit_dg(GemvParams p_in) {
+  const GemvParams p = load_params(p_in);
+  constexpr int kPieces = 16;   // the 256-B-entry (WT) table: 32 bank-private 8-B copies, one v_perm per address
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[2 * kTabDwords];
+  __shared__ float s_code2[256];
+  __shared__ float s_red[NWK][R][16];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int row0 = blockIdx.x * R;
+  const int m = lane & 15;                                   // this lane's C column = its diagonal row
+  const uint32_t c = 4u * (uint32_t)m + ((uint32_t)lane >> 4);  // this lane's 16-element chunk of a segment
+  const uint32_t row_bytes = (uint32_t)p.K >> 1;
+  // 1. code2 and the table entry first (the barrier waits for them)
+  float c2 = 0.0f;
+  if (threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x];
+  const float offset = *p.sc.offset;
+  u32x4 tab_entry = {0u, 0u, 0u, 0u};
+  if (threadIdx.x < 256) tab_entry = reinterpret_cast<const u32x4 *>((CL ? &g_byte_tab_nf4x : &g_byte_tab_nf4)->v)[threadIdx.x];
+  // 2. weights (R rows x NSEG segments), x (the lane's chunk of each segment), scale codes
+  const uint32_t seg0 = (uint32_t)(wave * NSEG);               // this wave's first segment of the row
+  u32x2 wv[NSEG][R];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned char *rp = p.B + (size_t)(uint32_t)(row0 + r) * row_bytes + (seg0 + sg) * 512u + 8u * c;
+      wv[sg][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(rp));
+    }
+  u32x4 xr[NSEG][2];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    const u32x4 *xp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(p.x) + ((seg0 + sg) * 1024u + 16u * c) * 2u);
+    xr[sg][0] = xp[0];
+    xr[sg][1] = xp[1];
+  }
+  const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;             // 64-element blocks per row
+  uint32_t qb[NSEG][R];
+  float a2[NSEG][R];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t b = (uint32_t)p.block_base + (uint32_t)(row0 + r) * bpr + (seg0 + sg) * 16u;   // the segment's first block
+      qb[sg][r] = p.sc.qabsmax[b + (uint32_t)m];
+      typedef const __attribute__((address_space(4))) float *cfp;
+      a2[sg][r] = ((cfp)p.sc.absmax2)[b >> p.bs2_log2];        // one per (row, segment): 16 | 256
+    }
+  if (threadIdx.x < 256) {
+    s_code2[threadIdx.x] = c2;
+    store_byte_table_entry<kPieces>(s_tab, tab_entry);
+  }
+  __syncthreads();
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  const uint32_t jb = (uint32_t)(lane & 31) << 3;
+  float4_t acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    const uint32_t X[8] = {xr[sg][0].x, xr[sg][0].y, xr[sg][0].z, xr[sg][0].w,
+                           xr[sg][1].x, xr[sg][1].y, xr[sg][1].z, xr[sg][1].w};
+    half8_t bfr[CL ? 4 : 2];
+#pragma unroll
+    for (int f = 0; f < (CL ? 4 : 2); ++f) {
+      const u32x4 b = CL ? u32x4{X[2 * f], X[2 * f], X[2 * f + 1], X[2 * f + 1]}
+                         : u32x4{X[4 * f], X[4 * f + 1], X[4 * f + 2], X[4 * f + 3]};
+      bfr[f] = __builtin_bit_cast(half8_t, b);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t w[2] = {wv[sg][r].x, wv[sg][r].y};
+      float4_t cc = {0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (CL) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const uint32_t wd = w[f >> 1];
+          const uint32_t b0 = (uint32_t)(2 * (f & 1)), b1 = b0 + 1u;
+          const u32x2 e0 = *reinterpret_cast<const u32x2 *>(tb + __builtin_amdgcn_perm(wd, jb, 0x0C0C0000u | ((4u + b0) << 8)));
+          const u32x2 e1 = *reinterpret_cast<const u32x2 *>(tb + __builtin_amdgcn_perm(wd, jb, 0x0C0C0000u | ((4u + b1) << 8)));
+          const u32x4 a = {e0.x, e0.y, e1.x, e1.y};
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), bfr[f], cc, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          uint32_t h[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            h[t] = *reinterpret_cast<const uint32_t *>(tb + __builtin_amdgcn_perm(w[f], jb, 0x0C0C0000u | ((4u + t) << 8)));
+          const u32x4 a = {h[0], h[1], h[2], h[3]};
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), bfr[f], cc, 0, 0, 0);
+        }
+      }
+      const float am = __fadd_rn(__fmul_rn(s_code2[qb[sg][r]], a2[sg][r]), offset);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[r][k] = fmaf(cc[k], am, acc[r][k]);
+    }
+  }
+  // the diagonal: lane l keeps register m & 3 if m >> 2 == l >> 4 (its block's dot), else nothing
+  const bool diag = (m >> 2) == (lane >> 4);
+  const int k3 = m & 3;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float v = k3 == 0 ? acc[r][0] : k3 == 1 ? acc[r][1] : k3 == 2 ? acc[r][2] : acc[r][3];
+    if (diag) s_red[wave][r][m] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < R * 16) {   // thread (r, b): the NWK partials of block column b of row r, then 16 lanes
+    const int r = threadIdx.x >> 4, b = threadIdx.x & 15;
+    float v = 0.0f;
+#pragma unroll
+    for (int wk = 0; wk < NWK; ++wk) v += s_red[wk][r][b];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+    if (b == 0) {
+      const int row = row0 + r;
+      float o = v * p.out_scale;
+      if (p.bias) o += load_f32<QZ_DT_F16>(p.bias, row);
+      store_f32<QZ_DT_F16>(p.y, row, o);
+    }
+  }
 }
 
 // Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
@@ -1679,6 +1982,10 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   p->nw = nullptr;
   p->eps = 0.0f;
   p->res = nullptr;
+  p->pf = nullptr;
+  p->pf_row_bytes = 0;
+  p->pf_rows = 0;
+  p->pf_chunks = 0;
   *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
             (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
             (long long)M * K + 2LL * 1024 < (1LL << 32) &&            // 32-bit element offsets

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def timed(fn, calls=50, reps=5):
+def timed(fn, calls=50, reps=5, all_reps=None):
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -40,10 +40,12 @@ def timed(fn, calls=50, reps=5):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
+        if all_reps is not None:
+            all_reps.append(round(dt / calls * 1e6, 2))
     return round(best / calls * 1e6, 2)
 
 
-def worker(rank, world, port, backend):
+def worker(rank, world, port, backend, reverse=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
@@ -51,16 +53,21 @@ def worker(rank, world, port, backend):
     dev = torch.device("cuda", 0)
     ag = OneShotAllGather(slot_bytes=1 << 17, device=dev)
     res = {}
-    for nbytes in (256, 1024, 2048, 4096, 7168, 16384, 65536):
+    sizes = (256, 1024, 2048, 4096, 7168, 16384, 65536)
+    order = list(reversed(sizes)) if reverse else list(sizes)
+    for nbytes in order:
         n = nbytes // 2
         x = torch.randn(n, device=dev).half()
         out = torch.empty(world * n, device=dev, dtype=torch.float16)
-        row = {"flags": timed(lambda: ag(out, x, 1)), "granules": timed(lambda: ag(out, x, 2))}
+        fr, gr = [], []
+        row = {"flags": timed(lambda: ag(out, x, 1), all_reps=fr), "granules": timed(lambda: ag(out, x, 2), all_reps=gr)}
+        row["flags_reps"], row["granules_reps"] = fr, gr
         if world == 1:
             row["rccl"] = timed(lambda: dist.all_gather_into_tensor(out, x))
         res[nbytes] = row
     if rank == 0:
-        print(json.dumps({"world": world, "us_per_call": res, "failed": ag.failed()}), flush=True)
+        print(json.dumps({"world": world, "order": "descending" if reverse else "ascending", "us_per_call": res,
+                          "failed": ag.failed()}), flush=True)
     dist.barrier()
     ag.close()
     dist.destroy_process_group()
@@ -69,10 +76,11 @@ def worker(rank, world, port, backend):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--reverse", action="store_true", help="measure the payload sizes largest first")
     a = ap.parse_args()
     import socket
     sk = socket.socket(); sk.bind(("127.0.0.1", 0)); port = sk.getsockname()[1]; sk.close()
     if a.world == 1:
-        worker(0, 1, port, "nccl")
+        worker(0, 1, port, "nccl", a.reverse)
     else:
-        mp.start_processes(worker, args=(a.world, port, "gloo"), nprocs=a.world, join=True, start_method="spawn")
+        mp.start_processes(worker, args=(a.world, port, "gloo", a.reverse), nprocs=a.world, join=True, start_method="spawn")

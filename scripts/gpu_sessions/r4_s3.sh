@@ -14,6 +14,10 @@ step() {  # name timeout cmd...
   [ $rc -eq 0 ] || exit $rc
 }
 step r4c_stamps 200 ./scripts/microbench/gemv_micro 4096 4096 9 stamps
+for s in "4096 4096" "14336 4096" "28672 4096" "6144 4096"; do
+  set -- $s
+  step r4c_mf_$1x$2 200 ./scripts/microbench/gemv_micro $1 $2 7 mf
+done
 step r4c_tests 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu \
   tests/test_gpu_mlp_pair.py tests/test_gpu_residual.py tests/test_gpu_decode_attention.py tests/test_gpu_prenorm.py \
   tests/test_gpu_xgmi_rowsplit.py tests/test_gpu_xgmi_exchange.py

@@ -448,6 +448,44 @@ int main(int argc, char **argv) {
     GVO(1, true, 0); GVO(1, true, 3);
     check_outputs("R=2 CL=true OPT=0");
   }
+  const bool mf = argc > 4 && std::string(argv[4]) == "mf";
+  // MFMA-product GEMV (k_gemv_4bit_mf, K = 4096 only): 16-row tiles, 8 waves split K, 4 loads each
+#define GVMF(CL_, WT_) timeit("mf CL=" #CL_ " WT=" #WT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.out_scale = (CL_) ? 1.0f / 16384 : 1.0f; \
+    hipLaunchKernelGGL((k_gemv_4bit_mf<CL_, WT_, 8, 4>), dim3(M / 16), dim3(512), 0, 0, q); })
+#define GVXL(R) timeit("gemvXL CL R=" #R " (x staged in LDS)", [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, true, 0, true, true>), dim3(g), dim3(256), K * 2, 0, q); })
+  const bool pf = argc > 4 && std::string(argv[4]) == "pf";
+  // launch i prefetches the first CHUNKS KiB of every row of launch i + 1's weights (the next copy)
+#define GVPF(R, CHUNKS) timeit("gemvFS CL R=" #R " prefetch next chunks=" #CHUNKS, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384; \
+    q.pf = P[(i + 1) % NC]; q.pf_row_bytes = (uint32_t)(K / 2); q.pf_rows = M; q.pf_chunks = CHUNKS; \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, true, false, 0, 0, true>), dim3(g), dim3(256), 0, 0, q); })
+  if (pf) {
+    GVO(2, true, 0); GVPF(2, 1); GVPF(2, 2); GVO(4, true, 0); GVPF(4, 1);
+    check_outputs("R=2 CL=true OPT=0");
+  }
+  const bool dg = argc > 4 && std::string(argv[4]) == "dg";
+  // MFMA-diagonal GEMV (k_gemv_4bit_dg, K = 1024 NSEG NWK): the product's row-contiguous loads
+#define GVDG(CL_, R, NSEG, NWK) timeit("dg CL=" #CL_ " R=" #R " NSEG=" #NSEG " NWK=" #NWK, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.out_scale = (CL_) ? 1.0f / 16384 : 1.0f; \
+    hipLaunchKernelGGL((k_gemv_4bit_dg<CL_, R, NSEG, NWK>), dim3(M / R), dim3(NWK * 64), 0, 0, q); })
+  if (dg && K == 4096) {
+    GVO(2, true, 0); GVO(2, false, 0);
+    GVDG(true, 8, 1, 4); GVDG(false, 8, 1, 4); GVDG(true, 4, 1, 4); GVDG(true, 2, 1, 4); GVDG(true, 4, 2, 2);
+    check_outputs("R=2 CL=true OPT=0");
+  }
+  if (mf && K == 4096) {
+    GVO(2, true, 0); GVO(2, false, 0);
+    GVMF(true, false); GVMF(true, true); GVMF(false, false);
+    GVXL(2); GVXL(4); GVXL(1);
+    check_outputs("R=2 CL=true OPT=0");
+  }
   const bool stream = argc > 4 && std::string(argv[4]) == "stream";
 #define GVST(R, G, CL_) timeit("stream2 R=" #R " wgs=" #G " CL=" #CL_, [&, pt = p](int i) { \
     GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
@@ -461,7 +499,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

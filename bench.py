@@ -540,7 +540,7 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 
 @torch.inference_mode()
-def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10):
+def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1):
     """The Linear4bit chain of a Llama-3-8B decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
@@ -548,13 +548,16 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10):
     graph: algorithmic bytes / time for the chain, i.e. the single-launch roofline with the
     dependent-launch gaps of a real decode step included (the attention launch between q/k/v and
     o_proj is left out: it is not a Linear4bit; o_proj reads the q output in its place, so every
-    launch still depends on the previous one)."""
+    launch still depends on the previous one).  shards = P > 1: the same chain on ONE rank's rows
+    of the row-split layout (every projection M / P rows, the launches a rank runs per layer at
+    N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
     from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
 
     dev = torch.device("cuda")
     torch.manual_seed(11)
     base = {}
     for name, (M, K) in zip(("q", "k", "v", "o", "gate", "up", "down"), LAYER_SHAPES):
+        M //= shards
         W = (torch.randn(M, K, device=dev) * 0.02).to(torch.float16)
         base[name] = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
         del W
@@ -568,19 +571,27 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10):
     sets = [{n: clone(*base[n]) for n in base} for _ in range(copies)]
     del base
     H, I = 4096, 14336
+    Hs, Is, KVs = H // shards, I // shards, 1024 // shards    # this rank's rows
     nw1 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
     nw2 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
     x0 = torch.randn(1, 1, H, device=dev).half()
-    qkv_out = [torch.empty(H, device=dev, dtype=torch.float16), torch.empty(1024, device=dev, dtype=torch.float16),
-               torch.empty(1024, device=dev, dtype=torch.float16)]
+    qkv_out = [torch.empty(Hs, device=dev, dtype=torch.float16), torch.empty(KVs, device=dev, dtype=torch.float16),
+               torch.empty(KVs, device=dev, dtype=torch.float16)]
+    # stand-ins for the exchanged full vectors a rank's next launch reads (row-split: every launch
+    # consumes the all-gathered [H] / [I] vector; P = 1: the previous output itself)
+    full_h = torch.randn(1, 1, I, device=dev).half()
 
     def layer(x, w):
         q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
                                         (*w["v"], None, 0, qkv_out[2])], exact_codes=True, norm=(nw1, 1e-5))
-        a = gemv_4bit(q.view(1, 1, H), w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1))
-        h = gemv_4bit_pair_silu(a, [(*w["gate"], None), (*w["up"], None)], exact_codes=True, norm=(nw2, 1e-5))
+        xo = q.view(1, 1, H) if shards == 1 else x          # o_proj reads the (gathered) attention output
+        a = gemv_4bit(xo, w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1)[:Hs])
+        xa = a if shards == 1 else x                        # ... the gathered residual stream
+        h = gemv_4bit_pair_silu(xa, [(*w["gate"], None), (*w["up"], None)], exact_codes=True, norm=(nw2, 1e-5))
         assert h is not None
-        return gemv_4bit(h, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1))
+        xh = h if shards == 1 else full_h                   # ... the gathered h
+        y = gemv_4bit(xh, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1)[:Hs])
+        return y if shards == 1 else x
 
     def chain():
         x = x0
@@ -609,17 +620,19 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10):
     us = statistics.median(times)
     # algorithmic bytes per layer: the four launches' GEMV bytes, + the two norm
     # weights and the two residual reads, - the pair's second output (it writes h only)
-    nbytes = (gemv_alg_bytes([(H, H), (1024, H), (1024, H)]) - 2 * (2 * H)   # q/k/v: x read once, not 3 x
-              + gemv_alg_bytes([(H, H)]) + 2 * H                                # o_proj + its residual read
-              + gemv_alg_bytes([(I, H)] * 2) - 2 * H - 2 * I                    # pair: x once, one [I] output
-              + gemv_alg_bytes([(H, I)]) + 2 * H                                # down_proj + its residual read
+    nbytes = (gemv_alg_bytes([(Hs, H), (KVs, H), (KVs, H)]) - 2 * (2 * H)   # q/k/v: x read once, not 3 x
+              + gemv_alg_bytes([(Hs, H)]) + 2 * Hs                              # o_proj + its residual read
+              + gemv_alg_bytes([(Is, H)] * 2) - 2 * H - 2 * Is                  # pair: x once, one output
+              + gemv_alg_bytes([(Hs, I)]) + 2 * Hs                              # down_proj + its residual read
               + 2 * (2 * H))                                                    # the two RMSNorm weights
     del sets, g
     torch.cuda.empty_cache()
     ach = nbytes / (us * 1e-6) / 1e9
     return {"what": "one Llama-3-8B layer's Linear4bit chain: q/k/v+norm grouped, o_proj+residual, gate/up+SiLU+norm "
                     "pair, down_proj+residual (4 dependent launches), NF4+DQ exact codes, one HIP graph of "
-                    f"{layers} layers over {copies} rotating weight sets",
+                    f"{layers} layers over {copies} rotating weight sets"
+                    + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
+            "shards": shards,
             "us_per_layer": round(us, 3), "us_per_launch": round(us / 4, 3), "algorithmic_bytes_per_layer": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_layer_min": round(min(times), 3), "us_per_layer_max": round(max(times), 3)}
@@ -983,6 +996,8 @@ def main():
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--chain-only", action="store_true",
                     help="only the Linear4bit chain of one decoder layer (chain_roofline; profiling)")
+    ap.add_argument("--chain-shards", type=int, default=1,
+                    help="--chain-only: the chain on one rank's rows of a P-way row split")
     ap.add_argument("--dominant-only", action="store_true",
                     help="only the grouped gate/up GEMV measurement (the decode step's longest launch; profiling)")
     ap.add_argument("--no-prefill", action="store_true")
@@ -1078,7 +1093,7 @@ def main():
         print(json.dumps(dominant_roofline()), flush=True)
         return
     if args.chain_only:
-        print(json.dumps(chain_roofline()), flush=True)
+        print(json.dumps(chain_roofline(shards=args.chain_shards)), flush=True)
         return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)

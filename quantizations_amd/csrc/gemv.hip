@@ -648,6 +648,37 @@ __device__ __forceinline__ float chunk_dot_tab_fm(const u32x4 &wv, const uint32_
   return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+// Exact codes against fp32 x (XF, round 4): the fp16 x of a step is widened to fp32 once (shared by
+// the wave's R rows) and each packed byte's fp32 code pair {code(hi nibble), code(lo nibble)} (the
+// kRawF32 table) meets its x pair in full-rate fp32 FMAs: PK = 0 two v_fma_f32, PK = 1 one
+// v_pk_fma_f32.  The products are fp32 (exact code x exact x, rounded once), as the reference's fp32
+// FMA chain (kernels.cu:1169-1210).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+template <int PK>
+__device__ __forceinline__ float chunk_dot_tab_xf(const u32x4 &wv, const f32x2_t (&xf)[16], const uint32_t *s_tab,
+                                                  uint32_t jb) {
+  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
+  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
+  f32x2_t s[2] = {f32x2_t{0.0f, 0.0f}, f32x2_t{0.0f, 0.0f}};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
+                           ((w[d] >> 9) & 0x7F80u) | jb, ((w[d] >> 17) & 0x7F80u) | jb};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f32x2_t e = *reinterpret_cast<const f32x2_t *>(tb + a[m]);
+      f32x2_t &acc = s[m & 1];
+      if constexpr (PK) {
+        asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(e), "v"(xf[4 * d + m]));
+      } else {
+        acc.x = fmaf(e.x, xf[4 * d + m].x, acc.x);
+        acc.y = fmaf(e.y, xf[4 * d + m].y, acc.y);
+      }
+    }
+  }
+  return (s[0].x + s[1].x) + (s[0].y + s[1].y);
+}
+
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
 // (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
 // readlane round trips through SGPRs.
@@ -917,13 +948,24 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // FMV (exact codes, fp16 x): 0 = hi + lo fp16 code pairs by v_dot2c; 1 = fp32 codes by
   // v_fma_mix_f32 (chunk_dot_tab_fm), two-VALU addresses; 2 = the same on the 256-B-entry (WT)
   // table with one-SDWA addresses
-  constexpr bool kFM = CL && DT == QZ_DT_F16 && FMV != 0;
+  constexpr bool kFM = CL && DT == QZ_DT_F16 && (FMV == 1 || FMV == 2);
+  // FMV 3 / 4: fp32 codes against x widened to fp32 once per step, v_fma_f32 / v_pk_fma_f32
+  // (chunk_dot_tab_xf); the 128-B-entry kRawF32 table, two-VALU addresses
+  constexpr bool kXF = CL && DT == QZ_DT_F16 && (FMV == 3 || FMV == 4);
   static_assert(FMV != 2 || WT, "SDWA addresses index the 256-B-entry table");
   // OPT (round 4): bit 0 = issue the wave's second K-step before the prologue barrier (both steps
   // of a K = 4096 row in flight from the start); bit 1 = build the fp16 byte-table entry from the
   // SGPR byte planes (tab / tab_lo) instead of loading it (no global load gates the barrier)
   constexpr bool kEarly = (OPT & 1) != 0;
   constexpr bool kSTab = (OPT & 2) != 0 && MODE == kModeTab && !kBF && !kF32 && !kFM;
+  // bit 2: the scale codes / absmax2 of a step become visible only inside consume() (an empty asm),
+  // so hipcc cannot hoist their use -- and the vmcnt wait it needs -- above the next step's issue
+  constexpr bool kLaunder = (OPT & 4) != 0;
+  // bit 3: the wave owns exactly two K-steps (host-checked): straight-line code -- issue, barrier,
+  // issue step 2, decode, decode -- with no loop whose shared dominator would take the waits of
+  // step 1's scale codes above step 2's issue (hipcc did: the product's K = 4096 waves waited for
+  // ALL of step 1 before issuing step 2)
+  constexpr bool kTwo = (OPT & 8) != 0;
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
@@ -989,7 +1031,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   } else if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
     static_assert(NW * 64 >= 256, "one byte-table entry per thread");
     if (!p.lut && threadIdx.x < 256) {
-      const ByteTable *bt = (kF32 || kFM) ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
+      const ByteTable *bt = (kF32 || kFM || kXF) ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
                             : kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
                                   : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
       tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
@@ -1034,7 +1076,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const bool have = s < nsteps;
   const int n_my = have ? (nsteps - wk + WK - 1) / WK : 0;  // this wave's steps: s = wk, wk + WK, ...
   if constexpr (kEarly) {
-    if (n_my >= 2) other.issue(p, row0, s + WK, lane, row_bytes);
+    // unconditional (a clamped step when there is no second one): a conditional issue makes hipcc's
+    // waitcnt before the table stores count only the loads common to both paths, i.e. wait for step 0
+    other.issue(p, row0, n_my >= 2 ? s + WK : (s < nsteps ? s : 0), lane, row_bytes);
   }
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
@@ -1075,7 +1119,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // runtime codebook (always exact codes) 2^-S of its in-kernel split
   float out_scale = p.out_scale;
   if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if constexpr (kF32 || kFM) {
+    if constexpr (kF32 || kFM || kXF) {
       if (p.lut) {
         out_scale = 1.0f;
         build_byte_table_f32<NW * 64, kPieces>(s_tab, p.lut);
@@ -1135,6 +1179,13 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // serialises HBM traffic with the decode.)
   typedef StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> Loads;
   auto consume = [&](const Loads &c) {
+    if constexpr (kLaunder) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        asm volatile("" : "+v"(const_cast<Loads &>(c).q[r]));
+        asm volatile("" : "+v"(const_cast<Loads &>(c).a[r]));
+      }
+    }
     if constexpr (XL) const_cast<Loads &>(c).xs.load_lds(s_x, c.xb);
     if constexpr (NRM) {
       auto &raw = const_cast<Loads &>(c).xs.raw;
@@ -1148,6 +1199,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     uint32_t hi[16], lo[kSplit ? 16 : 1];
     float usc;
     c.xs.prepare(hi, lo, usc);
+    f32x2_t xf[kXF ? 16 : 1];
+    if constexpr (kXF) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const auto h = __builtin_bit_cast(h2_t, hi[i]);
+        xf[i] = f32x2_t{(float)h.x, (float)h.y};
+      }
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       float am;
@@ -1158,6 +1217,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       float d;
       if constexpr (kF32) d = chunk_dot_tab_f32(c.wv[r], c.xs.raw, s_tab, jb);
       else if constexpr (kFM) d = chunk_dot_tab_fm<FMV == 2 ? 1 : 0>(c.wv[r], hi, s_tab, jb, ad);
+      else if constexpr (kXF) d = chunk_dot_tab_xf<FMV == 4 ? 1 : 0>(c.wv[r], xf, s_tab, jb);
       else if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
       else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
       acc[r] = fmaf(d, am, acc[r]);
@@ -1186,7 +1246,14 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       }
     }
   };
-  if (kEarly && have) {
+  if constexpr (kTwo && !kEarly) {
+    other.issue(p, row0, s + WK, lane, row_bytes);
+    prefetch();
+    __builtin_amdgcn_sched_barrier(0);
+    consume(cur);
+    QZ_STAMP(2);
+    consume(other);
+  } else if (kEarly && have) {
     // `other` already holds step s + WK (n >= 2); at the loop top cur = step j, other = j + 1
     const int n = n_my;
     int j = 0;
@@ -1729,7 +1796,7 @@ struct GemvGroup {
   int nseg;
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false>
+template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false, int OPT = 0>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -1742,15 +1809,15 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, false, NRM>(seg, b - start);
+  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, false, NRM, false, 0, OPT>(seg, b - start);
 }
 
 // LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
-template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM>
+template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0>
 __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
-  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true>(seg, blockIdx.x, g.seg);
+  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true, 0, OPT>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -1850,18 +1917,30 @@ static int ilog2(long long v) {
 }
 
 // Geometries choose_geometry can return: (R, WK) in {(4,1), (4,2), (2,1), (1,1), (1,2), (1,4)}.
+// two_steps(K, WK): every wave owns exactly two full K-steps (gemv_body OPT 8, the straight-line
+// form: step 2 issued right after the prologue barrier; profiles/r4_gemv_two_step.txt)
+static inline bool two_steps(int K, int WK, bool fs) { return fs && K == 2 * 2048 * WK; }
+
 template <int MODE, bool DQ, int DT, bool FS, bool CL>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
-#define QZ_GV(RR, WW) \
-  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL>), dim3(grid), dim3(256), 0, s, p)
-  if (R == 4 && WK == 2) QZ_GV(4, 2);
-  else if (R == 4) QZ_GV(4, 1);
-  else if (R == 2) QZ_GV(2, 1);
-  else if (WK == 1) QZ_GV(1, 1);
-  else if (WK == 2) QZ_GV(1, 2);
-  else QZ_GV(1, 4);
+#define QZ_GV(RR, WW, OPT_) \
+  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL, false, 0, OPT_>), dim3(grid), dim3(256), 0, s, p)
+#define QZ_GV_RW(OPT_)                        \
+  do {                                        \
+    if (R == 4 && WK == 2) QZ_GV(4, 2, OPT_); \
+    else if (R == 4) QZ_GV(4, 1, OPT_);       \
+    else if (R == 2) QZ_GV(2, 1, OPT_);       \
+    else if (WK == 1) QZ_GV(1, 1, OPT_);      \
+    else if (WK == 2) QZ_GV(1, 2, OPT_);      \
+    else QZ_GV(1, 4, OPT_);                   \
+  } while (0)
+  if constexpr (FS) {
+    if (two_steps(p.K, WK, true)) { QZ_GV_RW(8); return; }
+  }
+  QZ_GV_RW(0);
+#undef QZ_GV_RW
 #undef QZ_GV
 }
 
@@ -2122,12 +2201,18 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   bool all_fs = true;
   for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;
-#define QZ_GR(DQ_, DT_, RR, WW, FS_)                                                                          \
+  const bool two = two_steps(K, WK, all_fs || nw);
+#define QZ_GR1(DQ_, DT_, RR, WW, FS_, OPT_)                                                                    \
   do {                                                                                                      \
-    if (cl) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, true>), dim3(blocks),  \
-                               dim3(256), 0, s, g);                                                         \
-    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, false>), dim3(blocks),    \
-                            dim3(256), 0, s, g);                                                            \
+    if (cl) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, true, false, OPT_>),   \
+                               dim3(blocks), dim3(256), 0, s, g);                                           \
+    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, false, false, OPT_>),     \
+                            dim3(blocks), dim3(256), 0, s, g);                                              \
+  } while (0)
+#define QZ_GR(DQ_, DT_, RR, WW, FS_)                                 \
+  do {                                                               \
+    if (FS_ && two) QZ_GR1(DQ_, DT_, RR, WW, FS_, (FS_ ? 8 : 0));    \
+    else QZ_GR1(DQ_, DT_, RR, WW, FS_, 0);                           \
   } while (0)
 #define QZ_GR_RW(DQ_, DT_, FS_)                                      \
   do {                                                               \
@@ -2144,9 +2229,13 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
     else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_);    \
     else QZ_GR_RW(DQ_, QZ_DT_F32, FS_);                              \
   } while (0)
-#define QZ_GN(DQ_, DT_, RR, WW, CL_)                                                                            \
-  hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true>), dim3(blocks), dim3(256), \
-                     (size_t)K * 2, s, g)
+#define QZ_GN(DQ_, DT_, RR, WW, CL_)                                                                          \
+  do {                                                                                                        \
+    if (two) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, 8>),          \
+                                dim3(blocks), dim3(256), (size_t)K * 2, s, g);                                \
+    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true>), dim3(blocks),  \
+                            dim3(256), (size_t)K * 2, s, g);                                                  \
+  } while (0)
 #define QZ_GN_RW(DQ_, DT_, CL_)                                      \
   do {                                                               \
     if (R == 4 && WK == 2) QZ_GN(DQ_, DT_, 4, 2, CL_);               \
@@ -2170,6 +2259,7 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
 #undef QZ_GR_DT
 #undef QZ_GR_RW
 #undef QZ_GR
+#undef QZ_GR1
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }
@@ -2234,8 +2324,14 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   for (int i = 2; i < kMaxSeg; ++i) g.start[i] = 0;
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = norm_weight ? (size_t)K * 2 : 0;
-#define QZ_PS(DQ_, DT_, RR, CL_, NRM_) \
-  hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_>), dim3(blocks), dim3(256), lds, s, g)
+  const bool two = two_steps(K, 1, true);
+#define QZ_PS(DQ_, DT_, RR, CL_, NRM_)                                                                               \
+  do {                                                                                                              \
+    if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8>), dim3(blocks), dim3(256), \
+                                lds, s, g);                                                                         \
+    else hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_>), dim3(blocks), dim3(256), lds, \
+                            s, g);                                                                                  \
+  } while (0)
 #define QZ_PS_R(DQ_, DT_, CL_, NRM_)           \
   do {                                          \
     if (R == 4) QZ_PS(DQ_, DT_, 4, CL_, NRM_);  \

@@ -441,6 +441,28 @@ int main(int argc, char **argv) {
     if (CL_) { q.out_scale = 1.0f / 16384; build_exact_planes(q.tab, q.tab_lo); } \
     const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
     hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, CL_, false, 0, OPT_>), dim3(g), dim3(256), 0, 0, q); })
+  // FMV 3 / 4: fp32 codes against x widened to fp32 once per step (v_fma_f32 / v_pk_fma_f32)
+  const bool xf = argc > 4 && std::string(argv[4]) == "xf";
+#define GVX(R, FMV_, OPT_) timeit("gemvFS CL R=" #R " FMV=" #FMV_ " OPT=" #OPT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.out_scale = (FMV_) ? 1.0f : 1.0f / 16384; q.tabsel = (FMV_) ? 0 : 2; \
+    if (!(FMV_)) build_exact_planes(q.tab, q.tab_lo); \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, true, false, FMV_, OPT_>), dim3(g), dim3(256), 0, 0, q); })
+  if (xf) {
+    GVFS(2, 0);                                      // fp16 codes (reference point)
+    if (K == 4096) {
+      GVX(2, 0, 8); GVX(2, 3, 8); GVX(2, 4, 8); GVX(4, 0, 8); GVX(4, 3, 8); GVX(4, 4, 8); GVX(1, 3, 8); GVX(1, 4, 8);
+    }
+    GVX(2, 0, 0); GVX(2, 3, 0); GVX(2, 4, 0); GVX(4, 0, 0); GVX(4, 3, 0); GVX(4, 4, 0); GVX(1, 4, 0);
+    check_outputs("FMV=0 OPT=0");
+  }
+  const bool two = argc > 4 && std::string(argv[4]) == "two";
+  if (two && K == 4096) {  // OPT 8: straight-line two-step waves (K = 4096, WK = 1)
+    GVO(2, true, 0); GVO(2, true, 8); GVO(2, true, 10); GVO(2, false, 0); GVO(2, false, 8); GVO(4, true, 0);
+    GVO(4, true, 8); GVO(1, true, 0); GVO(1, true, 8);
+    check_outputs("R=2 CL=true OPT=0");
+  }
   if (early) {
     GVO(2, true, 0); GVO(2, true, 1); GVO(2, true, 2); GVO(2, true, 3);
     GVO(2, false, 0); GVO(2, false, 1); GVO(2, false, 3);
@@ -499,7 +521,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf && !two && !xf) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);
@@ -579,6 +601,9 @@ int main(int argc, char **argv) {
       run("gemv tab DQ R=2 full-step exact codes, second step before the barrier (OPT 1)", g * 4, [&, pt = p](int i) {
         GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
         hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true, false, 0, 1>), dim3(g), dim3(256), 0, 0, q); });
+      run("gemv tab DQ R=2 full-step exact codes, straight-line two steps (OPT 8)", g * 4, [&, pt = p](int i) {
+        GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
+        hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, 2, 1, 4, false, 512, true, true, false, 0, 8>), dim3(g), dim3(256), 0, 0, q); });
       run("gemv tab DQ R=2 full-step exact codes, SGPR table (OPT 2)", g * 4, [&, pt = p](int i) {
         GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; q.out_scale = 1.0f / 16384;
         build_exact_planes(q.tab, q.tab_lo);

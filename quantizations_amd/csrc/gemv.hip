@@ -659,7 +659,8 @@ __device__ __forceinline__ float chunk_dot_tab_xf(const u32x4 &wv, const f32x2_t
                                                   uint32_t jb) {
   const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
   const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  f32x2_t s[2] = {f32x2_t{0.0f, 0.0f}, f32x2_t{0.0f, 0.0f}};
+  f32x2_t s2[2] = {f32x2_t{0.0f, 0.0f}, f32x2_t{0.0f, 0.0f}};
+  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
@@ -667,16 +668,19 @@ __device__ __forceinline__ float chunk_dot_tab_xf(const u32x4 &wv, const f32x2_t
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const f32x2_t e = *reinterpret_cast<const f32x2_t *>(tb + a[m]);
-      f32x2_t &acc = s[m & 1];
       if constexpr (PK) {
-        asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(e), "v"(xf[4 * d + m]));
+        asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(s2[m & 1]) : "v"(e), "v"(xf[4 * d + m]));
       } else {
-        acc.x = fmaf(e.x, xf[4 * d + m].x, acc.x);
-        acc.y = fmaf(e.y, xf[4 * d + m].y, acc.y);
+        // written out: hipcc would SLP-pack the pair into v_pk_fma_f32 (+ register copies), which
+        // issues no faster than the two full-rate FMAs it replaces
+        const float ex = e.x, ey = e.y, xx = xf[4 * d + m].x, xy = xf[4 * d + m].y;
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s[(2 * m) & 3]) : "v"(ex), "v"(xx));
+        asm("v_fmac_f32 %0, %1, %2" : "+v"(s[(2 * m + 1) & 3]) : "v"(ey), "v"(xy));
       }
     }
   }
-  return (s[0].x + s[1].x) + (s[0].y + s[1].y);
+  if constexpr (PK) return (s2[0].x + s2[1].x) + (s2[0].y + s2[1].y);
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan

@@ -926,7 +926,7 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
           bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0,
-          bool PF = false>
+          bool PF = false, bool PS = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
                                           const GemvParams *pair = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
@@ -970,10 +970,16 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // step 1's scale codes above step 2's issue (hipcc did: the product's K = 4096 waves waited for
   // ALL of step 1 before issuing step 2)
   constexpr bool kTwo = (OPT & 8) != 0;
+  // PS (round 4, pair launches): persistent workgroups -- the grid is smaller than the row blocks and
+  // each workgroup takes blocks blockIdx.x, + gridDim.x, ..., so its prologue (byte table, code2,
+  // the fused RMSNorm of x into LDS) is paid once for all of them; the next block's first step is
+  // issued before the current block's epilogue
+  static_assert(!PS || (PAIR && kTwo && !kEarly && !PF), "persistent form: two-step pair launches");
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
   __shared__ float s_part[NW][R];
+  __shared__ float s_part2[PS ? 2 : 1][NW][R];   // PS: by block parity (no barrier after the reads)
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? (WT ? 2 : 1) * kTabDwords : 1];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
 
@@ -983,7 +989,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int wk = wave % WK;
   const int rg = wave / WK;
-  const int row0 = PAIR ? (block * 2 + (wave & 1)) * R : (block * RG + rg) * R;
+  int row0 = PAIR ? (block * 2 + (wave & 1)) * R : (block * RG + rg) * R;
   const int cb = PAIR ? (wave >> 1) : 0;   // this wave's code2 table
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
@@ -1250,7 +1256,54 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       }
     }
   };
-  if constexpr (kTwo && !kEarly) {
+  if constexpr (PS) {
+    // the pair epilogue of block `blk` (the one after the loop below, with s_part by parity)
+    auto pair_out = [&](int blk, int par) {
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
+      if (lane == kWave - 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          float o = v[r] * out_scale;
+          if (p.bias) o += load_f32<DT>(p.bias, min(row0 + r, p.M - 1));
+          s_part2[par][wave][r] = o;
+        }
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < 2 * R) {
+        const int g2 = threadIdx.x / R, r = threadIdx.x % R;
+        const int row = (blk * 2 + g2) * R + r;
+        if (row < p.M) {
+          const float gv = round_store<DT>(s_part2[par][g2][r]), uv = round_store<DT>(s_part2[par][2 + g2][r]);
+          const float a = round_store<DT>(__fdiv_rn(gv, __fadd_rn(1.0f, expf(-gv))));
+          store_f32<DT>(keep_sp(pair[0].y), row, __fmul_rn(a, uv));
+        }
+      }
+    };
+    const int nblocks = (p.M + 2 * R - 1) / (2 * R);
+    int blk = block;
+    for (int it = 0;; ++it) {
+      other.issue(p, row0, s + WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(cur);
+      consume(other);
+      const int nb = blk + (int)gridDim.x;   // workgroup-uniform
+      if (nb >= nblocks) {
+        pair_out(blk, it & 1);
+        break;
+      }
+      const int nrow0 = (nb * 2 + (wave & 1)) * R;
+      cur.issue(p, nrow0, s, lane, row_bytes);   // the next block's first step, ahead of this epilogue
+      __builtin_amdgcn_sched_barrier(0);
+      pair_out(blk, it & 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+      blk = nb;
+      row0 = nrow0;
+    }
+    return;
+  } else if constexpr (kTwo && !kEarly) {
     other.issue(p, row0, s + WK, lane, row_bytes);
     prefetch();
     __builtin_amdgcn_sched_barrier(0);
@@ -1817,11 +1870,11 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
 }
 
 // LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
-template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0>
+template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0, bool PS = false>
 __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
-  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true, 0, OPT>(seg, blockIdx.x, g.seg);
+  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true, 0, OPT, false, PS>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -2329,10 +2382,30 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = norm_weight ? (size_t)K * 2 : 0;
   const bool two = two_steps(K, 1, true);
+  // Persistent workgroups (gemv_body PS) for two-step launches with the fused RMSNorm: every
+  // workgroup normalises x once for several row blocks instead of once per block (measured,
+  // profiles/r4_pair_persistent.txt: 14336 rows 19.5 -> 16.4 us, 7168 rows 13.9 -> 10.4 us, the
+  // N = 4 / 8 shards 8.9 -> 7.4 and 7.9 -> 6.3 us; without the norm the one-block-per-workgroup
+  // launch stays faster).  Grid: 3 workgroups per CU (what the 43 KiB LDS image admits), the best
+  // or within 4 % of the best of 2 / 3 / 4 per CU and of blocks / 2 at every shape.  QZ_PAIR_PS
+  // (measurement knob, read per call) overrides: 1..8 = workgroups per CU, >= 16 = the grid, 0 = one
+  // workgroup per block
+  const char *pse = getenv("QZ_PAIR_PS");
+  int pgrid_i = 0;
+  if (pse) {
+    const int ps = atoi(pse);
+    pgrid_i = ps <= 0 ? 0 : ps <= 8 ? 256 * ps : ps;
+  } else if (norm_weight) {
+    pgrid_i = 3 * 256;
+  }
+  const unsigned pgrid = (unsigned)max(pgrid_i, 1);
+  const bool persist = two && pgrid_i > 0 && pgrid_i < blocks;
 #define QZ_PS(DQ_, DT_, RR, CL_, NRM_)                                                                               \
   do {                                                                                                              \
-    if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8>), dim3(blocks), dim3(256), \
-                                lds, s, g);                                                                         \
+    if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8, true>), dim3(pgrid), \
+                                    dim3(256), lds, s, g);                                                          \
+    else if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8>), dim3(blocks),    \
+                                     dim3(256), lds, s, g);                                                         \
     else hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_>), dim3(blocks), dim3(256), lds, \
                             s, g);                                                                                  \
   } while (0)

@@ -48,6 +48,28 @@ def test_pair_silu_bit_identical_to_grouped_plus_product(dtype, exact, M, K, nor
     assert torch.equal(h, F.silu(gate) * up)
 
 
+@pytest.mark.parametrize("ps", [2, 3, 448])
+@pytest.mark.parametrize("M,norm,bias,dtype", [(14336, True, False, torch.float16), (14336, False, True, torch.float16),
+                                               (3002, True, True, torch.float16), (7168, True, False, torch.bfloat16)])
+def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm, bias, dtype):
+    """QZ_PAIR_PS: persistent pair workgroups (ps per CU, or a grid of ps; each taking blocks b, b + grid, ...) give
+    the one-workgroup-per-block launch's bits, ragged last block included (K = 4096: two-step waves)."""
+    from quantizations_amd.core import gemv_4bit_pair_silu
+
+    K = 4096
+    items = _items(M, K, dtype, seed=M + ps, bias=bias)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).to(dtype)
+    nrm = ((1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(dtype), 1e-5) if norm else None
+    monkeypatch.setenv("QZ_PAIR_PS", "0")
+    ref = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
+    monkeypatch.setenv("QZ_PAIR_PS", str(ps))
+    h = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
+    torch.cuda.synchronize()
+    assert ref is not None and h is not None
+    assert torch.equal(h, ref)
+
+
 def test_pair_silu_fp4_without_double_quant():
     from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
 

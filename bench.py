@@ -906,6 +906,7 @@ def setup_oneshot(rank: int):
         from quantizations_amd.exchange import OneShotAllGather
         g = OneShotAllGather(slot_bytes=1 << 18)
         if g.verify():
+            g.warm_graph()   # the process's first captured graph is the slow one (exchange.warm_graph)
             return g, "oneshot-ipc"
         log(f"[rank {rank}] one-shot all-gather disagrees with RCCL: using RCCL")
         return None, "rccl (one-shot failed verification)"

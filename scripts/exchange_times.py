@@ -45,7 +45,7 @@ def timed(fn, calls=50, reps=5, all_reps=None):
     return round(best / calls * 1e6, 2)
 
 
-def worker(rank, world, port, backend, reverse=False):
+def worker(rank, world, port, backend, reverse=False, granules_first=False, warm=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
@@ -53,6 +53,10 @@ def worker(rank, world, port, backend, reverse=False):
     dev = torch.device("cuda", 0)
     ag = OneShotAllGather(slot_bytes=1 << 17, device=dev)
     res = {}
+    if warm:  # a throwaway graph of flag-protocol calls before anything is timed
+        xw = torch.randn(512, device=dev).half()
+        ow = torch.empty(world * 512, device=dev, dtype=torch.float16)
+        timed(lambda: ag(ow, xw, 1), reps=2)
     sizes = (256, 1024, 2048, 4096, 7168, 16384, 65536)
     order = list(reversed(sizes)) if reverse else list(sizes)
     for nbytes in order:
@@ -60,13 +64,18 @@ def worker(rank, world, port, backend, reverse=False):
         x = torch.randn(n, device=dev).half()
         out = torch.empty(world * n, device=dev, dtype=torch.float16)
         fr, gr = [], []
-        row = {"flags": timed(lambda: ag(out, x, 1), all_reps=fr), "granules": timed(lambda: ag(out, x, 2), all_reps=gr)}
+        if granules_first:
+            row = {"granules": timed(lambda: ag(out, x, 2), all_reps=gr)}
+            row["flags"] = timed(lambda: ag(out, x, 1), all_reps=fr)
+        else:
+            row = {"flags": timed(lambda: ag(out, x, 1), all_reps=fr), "granules": timed(lambda: ag(out, x, 2), all_reps=gr)}
         row["flags_reps"], row["granules_reps"] = fr, gr
         if world == 1:
             row["rccl"] = timed(lambda: dist.all_gather_into_tensor(out, x))
         res[nbytes] = row
     if rank == 0:
-        print(json.dumps({"world": world, "order": "descending" if reverse else "ascending", "us_per_call": res,
+        print(json.dumps({"world": world, "order": "descending" if reverse else "ascending",
+                          "first": "granules" if granules_first else "flags", "warm_graph": warm, "us_per_call": res,
                           "failed": ag.failed()}), flush=True)
     dist.barrier()
     ag.close()
@@ -77,10 +86,12 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--reverse", action="store_true", help="measure the payload sizes largest first")
+    ap.add_argument("--granules-first", action="store_true", help="time the granule protocol before the flags one")
+    ap.add_argument("--warm", action="store_true", help="replay a throwaway flag-protocol graph before timing")
     a = ap.parse_args()
     import socket
     sk = socket.socket(); sk.bind(("127.0.0.1", 0)); port = sk.getsockname()[1]; sk.close()
     if a.world == 1:
-        worker(0, 1, port, "nccl", a.reverse)
+        worker(0, 1, port, "nccl", a.reverse, a.granules_first, a.warm)
     else:
-        mp.start_processes(worker, args=(a.world, port, "gloo", a.reverse), nprocs=a.world, join=True, start_method="spawn")
+        mp.start_processes(worker, args=(a.world, port, "gloo", a.reverse, a.granules_first, a.warm), nprocs=a.world, join=True, start_method="spawn")

@@ -49,6 +49,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <utility>
 
 namespace qz {
 
@@ -683,6 +684,15 @@ __device__ __forceinline__ float chunk_dot_tab_xf(const u32x4 &wv, const f32x2_t
   return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+// compile-time loop: f(std::integral_constant<int, 0>{}) .. f(<N - 1>)
+template <typename F, int... Ns>
+__device__ __forceinline__ void gv_static_for_impl(F &&f, std::integer_sequence<int, Ns...>) {
+  (f(std::integral_constant<int, Ns>{}), ...);
+}
+template <int N, typename F> __device__ __forceinline__ void gv_static_for(F &&f) {
+  gv_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
 // (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
 // readlane round trips through SGPRs.
@@ -926,7 +936,7 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
           bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0,
-          bool PF = false, bool PS = false>
+          bool PF = false, bool PS = false, int NSW = 0>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
                                           const GemvParams *pair = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
@@ -975,6 +985,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // the fused RMSNorm of x into LDS) is paid once for all of them; the next block's first step is
   // issued before the current block's epilogue
   static_assert(!PS || (PAIR && kTwo && !kEarly && !PF), "persistent form: two-step pair launches");
+  // bits 4 / 5 (round 4): a ring of 3 / 4 step buffers for waves that own exactly NSW K-steps
+  // (host-checked; K = 14336: Llama-3-8B down_proj, 7 steps), straight-line: step i + D - 1 is
+  // issued before step i is decoded, so D - 1 steps stay in flight instead of one
+  constexpr int kRing = (OPT & 32) ? 4 : (OPT & 16) ? 3 : 0;
+  static_assert(kRing == 0 || (NSW >= 2 && !kEarly && !kTwo && !PS && !PF), "ring: a fixed step count");
   constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
   constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
   __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
@@ -1256,7 +1271,31 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       }
     }
   };
-  if constexpr (PS) {
+  if constexpr (kRing > 0) {
+    Loads third, fourth;
+    auto sel = [&](auto K) -> Loads & {
+      constexpr int k = decltype(K)::value;
+      if constexpr (k == 0) return cur;
+      else if constexpr (k == 1) return other;
+      else if constexpr (k == 2) return third;
+      else return fourth;
+    };
+    gv_static_for<NSW>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i == 0) {
+        gv_static_for<kRing - 1>([&](auto J) {
+          constexpr int j = decltype(J)::value + 1;
+          if constexpr (j < NSW) sel(std::integral_constant<int, j % kRing>{}).issue(p, row0, s + j * WK, lane, row_bytes);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (i + kRing - 1 < NSW) {
+        constexpr int j = i + kRing - 1;
+        sel(std::integral_constant<int, j % kRing>{}).issue(p, row0, s + j * WK, lane, row_bytes);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      consume(sel(std::integral_constant<int, i % kRing>{}));
+    });
+  } else if constexpr (PS) {
     // the pair epilogue of block `blk` (the one after the loop below, with s_part by parity)
     auto pair_out = [&](int blk, int par) {
       float v[R];
@@ -1458,9 +1497,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
 }
 
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0, bool PF = false>
+          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0, bool PF = false, int NSW = 0>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT, PF>(p, blockIdx.x);
+  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT, PF, false, NSW>(p, blockIdx.x);
 }
 
 // Streaming ("persistent") form for rows of exactly NS K-steps (K = 2048 * NS, full-step

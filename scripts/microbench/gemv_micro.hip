@@ -457,6 +457,25 @@ int main(int argc, char **argv) {
     GVX(2, 0, 0); GVX(2, 3, 0); GVX(2, 4, 0); GVX(4, 0, 0); GVX(4, 3, 0); GVX(4, 4, 0); GVX(1, 4, 0);
     check_outputs("FMV=0 OPT=0");
   }
+  // OPT 16 / 32: a ring of 3 / 4 step buffers for waves owning exactly NSW steps (K = 2048 NSW, WK = 1)
+  const bool ring = argc > 4 && std::string(argv[4]) == "ring";
+#define GVR(R, OPT_, NSW_) timeit("gemvFS CL R=" #R " OPT=" #OPT_ " NSW=" #NSW_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.tabsel = 2; q.out_scale = 1.0f / 16384; build_exact_planes(q.tab, q.tab_lo); \
+    const unsigned g = (unsigned)((M + R * 4 - 1) / (R * 4)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, 4, false, 0, true, true, false, 0, OPT_, false, NSW_>), dim3(g), dim3(256), 0, 0, q); })
+  if (ring && K == 14336) {
+    GVO(2, true, 0); GVR(2, 16, 7); GVR(2, 32, 7); GVO(4, true, 0); GVR(4, 16, 7); GVR(4, 32, 7); GVO(1, true, 0); GVR(1, 16, 7); GVR(1, 32, 7);
+    check_outputs("R=2 CL=true OPT=0");
+  }
+  if (ring && K == 28672) {
+    GVO(2, true, 0); GVR(2, 16, 14); GVR(2, 32, 14); GVO(4, true, 0); GVR(4, 16, 14); GVR(4, 32, 14);
+    check_outputs("R=2 CL=true OPT=0");
+  }
+  if (ring && K == 8192) {
+    GVO(2, true, 0); GVR(2, 16, 4); GVR(2, 32, 4); GVO(4, true, 0); GVR(4, 16, 4);
+    check_outputs("R=2 CL=true OPT=0");
+  }
   const bool two = argc > 4 && std::string(argv[4]) == "two";
   if (two && K == 4096) {  // OPT 8: straight-line two-step waves (K = 4096, WK = 1)
     GVO(2, true, 0); GVO(2, true, 8); GVO(2, true, 10); GVO(2, false, 0); GVO(2, false, 8); GVO(4, true, 0);
@@ -521,7 +540,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf && !two && !xf) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf && !two && !xf && !ring) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

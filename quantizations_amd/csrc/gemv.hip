@@ -2014,8 +2014,11 @@ static int ilog2(long long v) {
 
 // Geometries choose_geometry can return: (R, WK) in {(4,1), (4,2), (2,1), (1,1), (1,2), (1,4)}.
 // two_steps(K, WK): every wave owns exactly two full K-steps (gemv_body OPT 8, the straight-line
-// form: step 2 issued right after the prologue barrier; profiles/r4_gemv_two_step.txt)
-static inline bool two_steps(int K, int WK, bool fs) { return fs && K == 2 * 2048 * WK; }
+// form: step 2 issued right after the prologue barrier; profiles/r4_gemv_two_step.txt).  WK = 1
+// only: at K = 8192, WK = 2 (the Llama-3-70B q/k/v and o shapes, R = 4) hipcc gives the
+// straight-line body 259-278 VGPRs against 130 for the loop form -- one wave per SIMD
+// (profiles/r4_bench_70b_two_step_regression.txt)
+static inline bool two_steps(int K, int WK, bool fs) { return fs && WK == 1 && K == 2 * 2048; }
 
 template <int MODE, bool DQ, int DT, bool FS, bool CL>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {

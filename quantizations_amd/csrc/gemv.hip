@@ -1909,11 +1909,20 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
 }
 
 // LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
-template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0, bool PS = false>
+template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0, bool PS = false, bool WT = false>
 __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
-  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, false, NRM, true, 0, OPT, false, PS>(seg, blockIdx.x, g.seg);
+  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, WT, NRM, true, 0, OPT, false, PS>(seg, blockIdx.x, g.seg);
+}
+
+// QZ_PAIR_WT (measurement knob): the persistent exact-code pair on the 256-B-entry table (64 KiB: 32
+// bank-private copies of each 8-B entry, v_perm addresses), 2 workgroups per CU
+template <bool DQ, int DT, int R, bool CL, bool NRM>
+static void launch_pair_wt(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
+  if constexpr (CL && NRM && DT == QZ_DT_F16 && (R == 2 || R == 4))
+    hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ, DT, R, true, CL, NRM, 8, true, true>), dim3(grid), dim3(256), lds,
+                       s, g);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -2432,19 +2441,29 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   // or within 4 % of the best of 2 / 3 / 4 per CU and of blocks / 2 at every shape.  QZ_PAIR_PS
   // (measurement knob, read per call) overrides: 1..8 = workgroups per CU, >= 16 = the grid, 0 = one
   // workgroup per block
+  // With exact codes and R = 2 / 4 the persistent pair takes the 256-B-entry table (64 KiB: 32
+  // bank-private copies of each 8-B entry, one v_perm per address, no bank conflicts) at 2
+  // workgroups per CU: 16.2-16.8 -> 15.1 us for 14336 rows, 10.8 -> 10.6 for 7168
+  // (profiles/r4_pair_persistent_wide_table.txt); QZ_PAIR_WT=0 (knob, read per call) keeps the 16-copy table
+  const char *wte = getenv("QZ_PAIR_WT");
+  // (from 3 blocks per workgroup on: at the N = 4 shard, 896 blocks, the 16-copy table at 3 per CU is
+  // 3 % faster)
+  const bool wt_ok = cl && norm_weight && (R == 2 || R == 4) && blocks >= 3 * 512 && !(wte && atoi(wte) == 0);
   const char *pse = getenv("QZ_PAIR_PS");
   int pgrid_i = 0;
   if (pse) {
     const int ps = atoi(pse);
     pgrid_i = ps <= 0 ? 0 : ps <= 8 ? 256 * ps : ps;
   } else if (norm_weight) {
-    pgrid_i = 3 * 256;
+    pgrid_i = (wt_ok ? 2 : 3) * 256;
   }
   const unsigned pgrid = (unsigned)max(pgrid_i, 1);
   const bool persist = two && pgrid_i > 0 && pgrid_i < blocks;
+  const bool pair_wt = persist && wt_ok;
 #define QZ_PS(DQ_, DT_, RR, CL_, NRM_)                                                                               \
   do {                                                                                                              \
-    if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8, true>), dim3(pgrid), \
+    if (pair_wt) launch_pair_wt<DQ_, DT_, RR, CL_, NRM_>(pgrid, lds, s, g);                                        \
+    else if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8, true>), dim3(pgrid), \
                                     dim3(256), lds, s, g);                                                          \
     else if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8>), dim3(blocks),    \
                                      dim3(256), lds, s, g);                                                         \

@@ -48,7 +48,9 @@ variants = [int(v) for v in os.environ.get("PAIR_PS", "0,2,3,4").split(",")]
 for nrm in ((w, 1e-5), None) if os.environ.get("PAIR_NONORM", "1") == "1" else ((w, 1e-5),):
     ref = None
     for ps in variants:
-        os.environ["QZ_PAIR_PS"] = str(ps)
+        os.environ["QZ_PAIR_PS"] = str(ps % 1000)
+        # 1000 + v: the 256-B-entry (WT) exact-code table at QZ_PAIR_PS = v; below 1000 the 16-copy one
+        os.environ["QZ_PAIR_WT"] = "1" if ps >= 1000 else "0"
         out = [gemv_4bit_pair_silu(x, copies[c], exact_codes=True, norm=nrm) for c in range(NC)]
         if ref is None:
             ref = out
@@ -59,3 +61,4 @@ for nrm in ((w, 1e-5), None) if os.environ.get("PAIR_NONORM", "1") == "1" else (
         if not same:
             sys.exit(3)
 os.environ["QZ_PAIR_PS"] = "0"
+os.environ.pop("QZ_PAIR_WT", None)

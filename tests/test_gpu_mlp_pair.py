@@ -49,6 +49,7 @@ def test_pair_silu_bit_identical_to_grouped_plus_product(dtype, exact, M, K, nor
 
 
 @pytest.mark.parametrize("ps", [2, 3, 448])
+@pytest.mark.filterwarnings("ignore")
 @pytest.mark.parametrize("M,norm,bias,dtype", [(14336, True, False, torch.float16), (14336, False, True, torch.float16),
                                                (3002, True, True, torch.float16), (7168, True, False, torch.bfloat16)])
 def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm, bias, dtype):
@@ -64,9 +65,15 @@ def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm,
     monkeypatch.setenv("QZ_PAIR_PS", "0")
     ref = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
     monkeypatch.setenv("QZ_PAIR_PS", str(ps))
+    for wt in ("0", "1"):   # the 16-copy and the 256-B-entry exact-code tables
+        monkeypatch.setenv("QZ_PAIR_WT", wt)
+        h = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
+        torch.cuda.synchronize()
+        assert ref is not None and h is not None
+        assert torch.equal(h, ref), wt
+    monkeypatch.delenv("QZ_PAIR_PS")
+    monkeypatch.delenv("QZ_PAIR_WT")   # the product default
     h = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
-    torch.cuda.synchronize()
-    assert ref is not None and h is not None
     assert torch.equal(h, ref)
 
 

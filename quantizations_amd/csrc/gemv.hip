@@ -934,11 +934,24 @@ __device__ __forceinline__ uint32_t norm_x_off(uint32_t chunk) {  // chunk = ele
   return (s << 12) + (l << 6) + ((i ^ ((l >> 2) & 3u)) << 4);
 }
 
+// Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
+// one decoder layer) in ONE grid.  Segment i owns row blocks
+// [start[i], start[i+1]); each segment keeps its own weights, statistics,
+// offset, bias and output, so every output is bit-identical to its own
+// qz_gemv_4bit launch with the same geometry.  total = all segments' blocks.
+constexpr int kMaxSeg = 4;
+struct GemvGroup {
+  GemvParams seg[kMaxSeg];
+  int start[kMaxSeg];
+  int nseg;
+  int total;
+};
+
 template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
           bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0,
-          bool PF = false, bool PS = false, int NSW = 0>
+          bool PF = false, bool PS = false, int NSW = 0, bool GPS = false>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
-                                          const GemvParams *pair = nullptr) {
+                                          const GemvParams *pair = nullptr, const GemvGroup *grp = nullptr) {
   // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
   static_assert(!NRM || (NW == 4 && FS && !XL && MODE == kModeTab && (DT == QZ_DT_F16 || DT == QZ_DT_BF16)),
                 "fused pre-norm: 4 waves, full steps, 16-bit activations");
@@ -985,6 +998,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // the fused RMSNorm of x into LDS) is paid once for all of them; the next block's first step is
   // issued before the current block's epilogue
   static_assert(!PS || (PAIR && kTwo && !kEarly && !PF), "persistent form: two-step pair launches");
+  // GPS (round 4, grouped launches with the fused norm): the same persistence over the blocks of all
+  // segments; a workgroup that crosses into another segment re-stages that segment's code2 table
+  static_assert(!GPS || (!PAIR && !PS && kTwo && !kEarly && !PF && WK == 1 && NW == 4), "grouped persistent form");
   // bits 4 / 5 (round 4): a ring of 3 / 4 step buffers for waves that own exactly NSW K-steps
   // (host-checked; K = 14336: Llama-3-8B down_proj, 7 steps), straight-line: step i + D - 1 is
   // issued before step i is decoded, so D - 1 steps stay in flight instead of one
@@ -1271,7 +1287,68 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       }
     }
   };
-  if constexpr (kRing > 0) {
+  if constexpr (GPS) {
+    auto seg_of = [&](int b) {
+      int sg = 0;
+#pragma unroll
+      for (int i = 1; i < kMaxSeg; ++i)
+        if (i < grp->nseg && b >= grp->start[i]) sg = i;
+      return __builtin_amdgcn_readfirstlane(sg);
+    };
+    auto store_rows = [&](const GemvParams &q, int r0) {
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
+      if (lane == kWave - 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int row = r0 + r;
+          if (row < q.M) {
+            float o = v[r] * out_scale;
+            if (q.bias) o += load_f32<DT>(q.bias, row);
+            o = add_res<DT>(o, q.res, row);
+            store_f32<DT>(q.y, row, o);
+          }
+        }
+      }
+    };
+    const int total = grp->total;
+    int blk = (int)blockIdx.x;
+    int sg = seg_of(blk);
+    GemvParams q = p;
+    for (int it = 0;; ++it) {
+      other.issue(q, row0, s + WK, lane, row_bytes);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(cur);
+      consume(other);
+      const int nb = blk + (int)gridDim.x;   // workgroup-uniform
+      if (nb >= total) {
+        store_rows(q, row0);
+        break;
+      }
+      const int ns = seg_of(nb);
+      const GemvParams qn = load_params(grp->seg[ns]);
+      const int nrow0 = ((nb - grp->start[ns]) * RG + rg) * R;
+      cur.issue(qn, nrow0, s, lane, row_bytes);   // the next block's first step, ahead of this epilogue
+      __builtin_amdgcn_sched_barrier(0);
+      store_rows(q, row0);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+      if (ns != sg) {   // another segment: its own code2 table and offset
+        if constexpr (DQ) {
+          __syncthreads();   // every wave has decoded the old segment's blocks
+          s_code2[0][threadIdx.x & 255] = qn.sc.code2[threadIdx.x & 255];
+          offset = *qn.sc.offset;
+          __syncthreads();
+        }
+        sg = ns;
+      }
+      q = qn;
+      blk = nb;
+      row0 = nrow0;
+    }
+    return;
+  } else if constexpr (kRing > 0) {
     Loads third, fourth;
     auto sel = [&](auto K) -> Loads & {
       constexpr int k = decltype(K)::value;
@@ -1880,19 +1957,9 @@ __global__ __launch_bounds__(NWK * 64) void k_gemv_4bit_dg(GemvParams p_in) {
   }
 }
 
-// Grouped launch: up to kMaxSeg GEMVs that share x and K (q/k/v, gate/up of
-// one decoder layer) in ONE grid.  Segment i owns workgroups
-// [start[i], start[i+1]); each segment keeps its own weights, statistics,
-// offset, bias and output, so every output is bit-identical to its own
-// qz_gemv_4bit launch with the same geometry.
-constexpr int kMaxSeg = 4;
-struct GemvGroup {
-  GemvParams seg[kMaxSeg];
-  int start[kMaxSeg];
-  int nseg;
-};
 
-template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false, int OPT = 0>
+template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false, int OPT = 0, bool GPS = false,
+          bool WT = false>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -1905,7 +1972,17 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, false, NRM, false, 0, OPT>(seg, b - start);
+  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, WT, NRM, false, 0, OPT, false, false, 0, GPS>(seg, b - start,
+                                                                                                 nullptr, &g);
+}
+
+// QZ_GROUPED_PS / QZ_GROUPED_WT (measurement knobs): persistent workgroups for the two-step grouped
+// launch with the fused norm (optionally on the 256-B-entry exact-code table)
+template <bool DQ, int DT, int R, bool CL, bool WT>
+static void launch_grouped_ps(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
+  if constexpr ((DT == QZ_DT_F16 || DT == QZ_DT_BF16) && (R == 1 || R == 2 || R == 4) && (!WT || (CL && DT == QZ_DT_F16)))
+    hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ, DT, R, 1, true, CL, true, 8, true, WT>), dim3(grid), dim3(256),
+                       lds, s, g);
 }
 
 // LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
@@ -2301,6 +2378,7 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
     blocks += (g.seg[i].M + rows_per_block - 1) / rows_per_block;
   }
   for (int i = nseg; i < kMaxSeg; ++i) g.start[i] = blocks;
+  g.total = blocks;
   // every workgroup repeats the norm prologue (x and the norm weight from L2, two barriers, 8 KiB
   // more LDS): past ~4096 workgroups it costs more than the separate launch saves (measured:
   // Llama-3-70B gate/up, 7168 workgroups, 74.6 us fused vs 58.6 us for the two launches;
@@ -2353,6 +2431,50 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
     else if (WK == 2) QZ_GN(DQ_, DT_, 1, 2, CL_);                    \
     else QZ_GN(DQ_, DT_, 1, 4, CL_);                                 \
   } while (0)
+  // QZ_GROUPED_PS (measurement knob, read per call): persistent workgroups for the two-step grouped
+  // launch with the fused norm: 1..8 per CU, >= 16 the grid; QZ_GROUPED_PS_R rows per wave (1, 2, 4)
+  // and QZ_GROUPED_WT=1 the 256-B-entry exact-code table
+  if (nw && two && WK == 1) {
+    const char *gpe = getenv("QZ_GROUPED_PS");
+    const int gps = gpe ? atoi(gpe) : 0;
+    if (gps > 0) {
+      int Rg = R;
+      if (const char *gre = getenv("QZ_GROUPED_PS_R")) {
+        const int v = atoi(gre);
+        if (v == 1 || v == 2 || v == 4) Rg = v;
+      }
+      GemvGroup g2 = g;
+      int gb = 0;
+      for (int i = 0; i < nseg; ++i) {
+        g2.start[i] = gb;
+        gb += (g2.seg[i].M + 4 * Rg - 1) / (4 * Rg);
+      }
+      for (int i = nseg; i < kMaxSeg; ++i) g2.start[i] = gb;
+      g2.total = gb;
+      const unsigned ggrid = (unsigned)(gps <= 8 ? 256 * gps : gps);
+      const char *gwe = getenv("QZ_GROUPED_WT");
+      const bool gwt = gwe && atoi(gwe) == 1 && cl && dtype == QZ_DT_F16;
+      if ((int)ggrid < gb) {
+        const size_t lds = (size_t)K * 2;
+#define QZ_GP(DQ_, DT_, RR)                                                                                 \
+  do {                                                                                                      \
+    if (gwt) launch_grouped_ps<DQ_, DT_, RR, true, true>(ggrid, lds, s, g2);                                \
+    else if (cl) launch_grouped_ps<DQ_, DT_, RR, true, false>(ggrid, lds, s, g2);                           \
+    else launch_grouped_ps<DQ_, DT_, RR, false, false>(ggrid, lds, s, g2);                                  \
+  } while (0)
+#define QZ_GP_R(DQ_, DT_)                                                                                   \
+  do {                                                                                                      \
+    if (Rg == 4) QZ_GP(DQ_, DT_, 4); else if (Rg == 2) QZ_GP(DQ_, DT_, 2); else QZ_GP(DQ_, DT_, 1);        \
+  } while (0)
+        if (dtype == QZ_DT_F16) { if (dq) QZ_GP_R(true, QZ_DT_F16); else QZ_GP_R(false, QZ_DT_F16); }
+        else { if (dq) QZ_GP_R(true, QZ_DT_BF16); else QZ_GP_R(false, QZ_DT_BF16); }
+#undef QZ_GP_R
+#undef QZ_GP
+        QZ_LAUNCH_CHECK();
+        return QZ_OK;
+      }
+    }
+  }
   if (nw) {
     if (dtype == QZ_DT_F16) {
       if (dq) { if (cl) QZ_GN_RW(true, QZ_DT_F16, true); else QZ_GN_RW(true, QZ_DT_F16, false); }

@@ -526,17 +526,17 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
     return {"kernel": ("k_gemv_4bit_pair gate/up + act_fn(gate) * up" if pair else "k_gemv_4bit_grouped gate/up")
                       + " 2 x 14336x4096 NF4+DQ (one launch per layer)"
                       + (", post-attention RMSNorm in its prologue" if prenorm else "")
-                      + (" (persistent workgroups, 3 per CU)" if (prenorm and pair) else ""),
+                      + (" (persistent workgroups, 2 per CU, 256-B-entry exact-code table)" if (prenorm and pair) else ""),
             "codes": "exact (fp32 as hi+lo fp16)" if prod else "fp16",
             "launch_us_avg": round(us, 3), "algorithmic_bytes": nbytes,
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "other_codes_launch_us": round(other_us, 3), "plain_grouped_launch_us": round(plain_us, 3),
-            "traffic": _pmc_traffic("r4_pair_persistent_pmc.json") if (prenorm and pair)
+            "traffic": _pmc_traffic("r4_pair_wide_pmc.json") if (prenorm and pair)
             else _pmc_traffic("r3_gateup_pmc.json"),
-            "profile": ("profiles/r4_pair_persistent_pmc.json (rocprofv3 FETCH/WRITE passes of THIS launch: the "
-                        "persistent pair with the norm and SiLU, exact codes; SQ counters "
-                        "profiles/r4_pair_persistent_sq_counters.txt, kernel trace r4_pair_persistent_trace_stats.txt)"
+            "profile": ("profiles/r4_pair_wide_pmc.json (rocprofv3 FETCH/WRITE passes of THIS launch: the "
+                        "persistent pair with the norm and SiLU, exact codes on the 256-B-entry table; SQ counters "
+                        "profiles/r4_pair_wide_sq_counters.txt, kernel trace r4_pair_wide_trace_stats.txt)"
                         if (prenorm and pair) else
                         "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the grouped "
                         "launch without the norm)")}

@@ -2124,6 +2124,18 @@ static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   if constexpr (FS) {
     if (two_steps(p.K, WK, true)) { QZ_GV_RW(8); return; }
   }
+  // exact codes, K >= 14336 (down_proj: 7 or more K-steps per wave): 8-wave workgroups sharing one
+  // 256-B-entry table (conflict-free, v_perm addresses): 4096 x 14336 8.92 -> 8.70 us, 8192 x 28672
+  // (R = 4) 29.2 -> 25.5 us (profiles/r4_gemv_8wave_wide_table.txt); the per-row sums are the same
+  if constexpr (FS && CL && DT == QZ_DT_F16 && MODE == kModeTab) {
+    const char *w8 = getenv("QZ_GEMV_WIDE8");   // measurement knob (read per call): 0 = off
+    if (WK == 1 && (R == 2 || R == 4) && p.K >= 14336 && !(w8 && atoi(w8) == 0)) {
+      const unsigned g8 = (unsigned)((p.M + R * 8 - 1) / (R * 8));
+      if (R == 4) hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, 4, 1, 8, false, 0, FS, CL, true>), dim3(g8), dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, 2, 1, 8, false, 0, FS, CL, true>), dim3(g8), dim3(512), 0, s, p);
+      return;
+    }
+  }
   QZ_GV_RW(0);
 #undef QZ_GV_RW
 #undef QZ_GV

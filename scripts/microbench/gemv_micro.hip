@@ -476,6 +476,23 @@ int main(int argc, char **argv) {
     GVO(2, true, 0); GVR(2, 16, 4); GVR(2, 32, 4); GVO(4, true, 0); GVR(4, 16, 4);
     check_outputs("R=2 CL=true OPT=0");
   }
+  // 8-wave workgroups sharing one 256-B-entry exact-code table (WT) vs the product (4 waves, 16-copy table)
+  const bool nw8 = argc > 4 && std::string(argv[4]) == "nw8";
+#define GVW(R, NW, WT_, OPT_) timeit("gemvFS CL R=" #R " NW=" #NW " WT=" #WT_ " OPT=" #OPT_, [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.tabsel = 2; q.out_scale = 1.0f / 16384; build_exact_planes(q.tab, q.tab_lo); \
+    const unsigned g = (unsigned)((M + R * NW - 1) / (R * NW)); \
+    hipLaunchKernelGGL((k_gemv_4bit<3, true, QZ_DT_F16, R, 1, NW, false, 0, true, true, WT_, 0, OPT_>), dim3(g), dim3(NW * 64), 0, 0, q); })
+  if (nw8) {
+    if (K == 4096) {
+      GVW(2, 4, false, 8); GVW(2, 8, true, 8); GVW(2, 8, false, 8); GVW(2, 4, true, 8); GVW(4, 8, true, 8); GVW(1, 8, true, 8);
+      check_outputs("R=2 NW=4 WT=false OPT=8");
+    } else {
+      GVW(2, 4, false, 0); GVW(2, 8, true, 0); GVW(2, 8, false, 0); GVW(2, 4, true, 0); GVW(4, 8, true, 0); GVW(1, 8, true, 0);
+      GVW(4, 4, false, 0);
+      check_outputs("R=2 NW=4 WT=false OPT=0");
+    }
+  }
   const bool two = argc > 4 && std::string(argv[4]) == "two";
   if (two && K == 4096) {  // OPT 8: straight-line two-step waves (K = 4096, WK = 1)
     GVO(2, true, 0); GVO(2, true, 8); GVO(2, true, 10); GVO(2, false, 0); GVO(2, false, 8); GVO(4, true, 0);
@@ -540,7 +557,7 @@ int main(int argc, char **argv) {
     GVST(1, 1024, false); GVST(8, 1024, false); GVST(8, 512, false);
     GVST(4, 1024, true); GVST(4, 768, true); GVST(2, 1024, true);
   }
-  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf && !two && !xf && !ring) {
+  if (!ablate && !small && !r8 && !tab && !tabab && !tabx && !tabfs && !tabxl && !skel && !tabab2 && !cl && !clsweep && !wt && !xcopy && !bf16 && !pk && !wk && !stream && !nopro && !wt8 && !fm && !early && !mf && !dg && !pf && !two && !xf && !ring && !nw8) {
   GV(1, true, 1, 1); GV(1, true, 2, 1); GV(1, true, 4, 1);
   GV(1, true, 1, 2); GV(1, true, 2, 2); GV(1, true, 4, 2);
   GV(1, true, 1, 4); GV(1, true, 2, 4); GV(1, true, 4, 4);

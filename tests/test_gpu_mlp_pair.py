@@ -77,6 +77,20 @@ def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm,
     assert torch.equal(h, ref)
 
 
+def test_pair_silu_persistent_fp4_without_double_quant(monkeypatch):
+    """The persistent pair (the default with the fused norm) on the FP4 codebook without double quant."""
+    from quantizations_amd.core import gemv_4bit_pair_silu
+
+    items = _items(14336, 4096, torch.float16, seed=21, quant="fp4", dq=False)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x = torch.randn(1, 1, 4096, device=DEV, generator=g).half()
+    nrm = ((1.0 + 0.1 * torch.randn(4096, device=DEV, generator=g)).half(), 1e-5)
+    monkeypatch.setenv("QZ_PAIR_PS", "0")
+    ref = gemv_4bit_pair_silu(x, items, norm=nrm)
+    monkeypatch.delenv("QZ_PAIR_PS")
+    assert torch.equal(gemv_4bit_pair_silu(x, items, norm=nrm), ref)
+
+
 def test_pair_silu_fp4_without_double_quant():
     from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
 

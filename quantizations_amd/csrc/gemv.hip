@@ -2111,7 +2111,8 @@ static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
 #define QZ_GV(RR, WW, OPT_) \
-  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL, false, 0, OPT_>), dim3(grid), dim3(256), 0, s, p)
+  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL, false, 0, (WW == 1 ? OPT_ : 0)>), dim3(grid), \
+                     dim3(256), 0, s, p)
 #define QZ_GV_RW(OPT_)                        \
   do {                                        \
     if (R == 4 && WK == 2) QZ_GV(4, 2, OPT_); \
@@ -2409,7 +2410,7 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   } while (0)
 #define QZ_GR(DQ_, DT_, RR, WW, FS_)                                 \
   do {                                                               \
-    if (FS_ && two) QZ_GR1(DQ_, DT_, RR, WW, FS_, (FS_ ? 8 : 0));    \
+    if (FS_ && two) QZ_GR1(DQ_, DT_, RR, WW, FS_, (FS_ && WW == 1 ? 8 : 0));    \
     else QZ_GR1(DQ_, DT_, RR, WW, FS_, 0);                           \
   } while (0)
 #define QZ_GR_RW(DQ_, DT_, FS_)                                      \
@@ -2427,9 +2428,16 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
     else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_);    \
     else QZ_GR_RW(DQ_, QZ_DT_F32, FS_);                              \
   } while (0)
+  // QZ_GROUPED_EARLY=1 (measurement knob, read per call): the normed two-step launch issues its second
+  // K-step before the prologue barriers (OPT 1 | 8) instead of after them
+  const char *gee = getenv("QZ_GROUPED_EARLY");
+  const bool g_early = gee && atoi(gee) == 1;
 #define QZ_GN(DQ_, DT_, RR, WW, CL_)                                                                          \
   do {                                                                                                        \
-    if (two) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, 8>),          \
+    if (two && g_early && WW == 1)                                                                            \
+      hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, (WW == 1 ? 9 : 0)>), dim3(blocks), \
+                         dim3(256), (size_t)K * 2, s, g);                                                     \
+    else if (two) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, (WW == 1 ? 8 : 0)>), \
                                 dim3(blocks), dim3(256), (size_t)K * 2, s, g);                                \
     else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true>), dim3(blocks),  \
                             dim3(256), (size_t)K * 2, s, g);                                                  \

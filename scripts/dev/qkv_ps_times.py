@@ -51,15 +51,16 @@ w = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).half()
 variants = os.environ.get("QKV_VARIANTS", "0:0:0,2:2:0,3:2:0,2:1:0,3:1:0,2:2:1,2:1:1,3:1:1").split(",")
 ref = None
 for v in variants:
-    ps, r, wt = v.split(":")
+    ps, r, wt, early = (v.split(":") + ["0"])[:4]
     os.environ["QZ_GROUPED_PS"], os.environ["QZ_GROUPED_PS_R"], os.environ["QZ_GROUPED_WT"] = ps, r, wt
+    os.environ["QZ_GROUPED_EARLY"] = early
     res = [[t.clone() for t in gemv_4bit_grouped(x, its[c], exact_codes=True, norm=(w, 1e-5))] for c in range(NC)]
     if ref is None:
         ref = res
     same = all(torch.equal(a, b) for ra, rb in zip(res, ref) for a, b in zip(ra, rb))
     t = graph_time(lambda i: gemv_4bit_grouped(x, its[i % NC], exact_codes=True, norm=(w, 1e-5)))
-    print(f"qkv {Ms}x{K} norm PS={ps} R={r} WT={wt}: {t:.2f} us/launch, bit-identical to the first: {same}", flush=True)
+    print(f"qkv {Ms}x{K} norm PS={ps} R={r} WT={wt} EARLY={early}: {t:.2f} us/launch, bit-identical to the first: {same}", flush=True)
     if not same:
         sys.exit(3)
-for k in ("QZ_GROUPED_PS", "QZ_GROUPED_PS_R", "QZ_GROUPED_WT"):
+for k in ("QZ_GROUPED_PS", "QZ_GROUPED_PS_R", "QZ_GROUPED_WT", "QZ_GROUPED_EARLY"):
     os.environ.pop(k, None)

@@ -543,23 +543,31 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 
 @torch.inference_mode()
-def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1):
-    """The Linear4bit chain of a Llama-3-8B decoder layer as the bench decode runs it -- q/k/v
+def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b"):
+    """The Linear4bit chain of a Llama-3 decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
-    `copies` rotating weight sets (8 x 113 MB > the 256 MiB Infinity Cache) captured in ONE HIP
-    graph: algorithmic bytes / time for the chain, i.e. the single-launch roofline with the
-    dependent-launch gaps of a real decode step included (the attention launch between q/k/v and
-    o_proj is left out: it is not a Linear4bit; o_proj reads the q output in its place, so every
-    launch still depends on the previous one).  shards = P > 1: the same chain on ONE rank's rows
-    of the row-split layout (every projection M / P rows, the launches a rank runs per layer at
-    N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
+    `copies` rotating weight sets (8B: 8 x 113 MB, 70B: 8 x 428 MB, both > the 256 MiB Infinity
+    Cache) captured in ONE HIP graph: algorithmic bytes / time for the chain, i.e. the
+    single-launch roofline with the dependent-launch gaps of a real decode step included (the
+    attention launch between q/k/v and o_proj is left out: it is not a Linear4bit; o_proj reads the
+    q output in its place, so every launch still depends on the previous one).  Where the product
+    takes another form (Llama-3-70B: gate/up at K = 8192 splits rows over two waves, so the pair
+    launch refuses and its norm prologue would exceed the workgroup cap), the chain runs what the
+    product runs: norm, grouped gate/up, SiLU product.  shards = P > 1: the same chain on ONE rank's
+    rows of the row-split layout (every projection M / P rows, the launches a rank runs per layer
+    at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
     from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
+    from quantizations_amd.layer_ops import silu_mul
 
+    base_cfg = MODELS[model_name]
+    H, I = base_cfg["hidden_size"], base_cfg["intermediate_size"]
+    KV = base_cfg["num_key_value_heads"] * (H // base_cfg["num_attention_heads"])
+    shapes = {"q": (H, H), "k": (KV, H), "v": (KV, H), "o": (H, H), "gate": (I, H), "up": (I, H), "down": (H, I)}
     dev = torch.device("cuda")
     torch.manual_seed(11)
     base = {}
-    for name, (M, K) in zip(("q", "k", "v", "o", "gate", "up", "down"), LAYER_SHAPES):
+    for name, (M, K) in shapes.items():
         M //= shards
         W = (torch.randn(M, K, device=dev) * 0.02).to(torch.float16)
         base[name] = quantize_4bit(W, blocksize=64, quant_type="nf4", compress_statistics=True)
@@ -573,16 +581,17 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
         return pk.clone(), st
     sets = [{n: clone(*base[n]) for n in base} for _ in range(copies)]
     del base
-    H, I = 4096, 14336
-    Hs, Is, KVs = H // shards, I // shards, 1024 // shards    # this rank's rows
+    Hs, Is, KVs = H // shards, I // shards, KV // shards    # this rank's rows
     nw1 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
     nw2 = (1.0 + 0.1 * torch.randn(H, device=dev)).half()
     x0 = torch.randn(1, 1, H, device=dev).half()
     qkv_out = [torch.empty(Hs, device=dev, dtype=torch.float16), torch.empty(KVs, device=dev, dtype=torch.float16),
                torch.empty(KVs, device=dev, dtype=torch.float16)]
+    gu_out = [torch.empty(Is, device=dev, dtype=torch.float16), torch.empty(Is, device=dev, dtype=torch.float16)]
     # stand-ins for the exchanged full vectors a rank's next launch reads (row-split: every launch
     # consumes the all-gathered [H] / [I] vector; P = 1: the previous output itself)
     full_h = torch.randn(1, 1, I, device=dev).half()
+    forms = set()
 
     def layer(x, w):
         q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
@@ -591,7 +600,13 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
         a = gemv_4bit(xo, w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1)[:Hs])
         xa = a if shards == 1 else x                        # ... the gathered residual stream
         h = gemv_4bit_pair_silu(xa, [(*w["gate"], None), (*w["up"], None)], exact_codes=True, norm=(nw2, 1e-5))
-        assert h is not None
+        if h is None:   # what the product runs where the pair launch refuses (fuse_layer_ops' MLP forward)
+            g_, u_ = gemv_4bit_grouped(xa, [(*w["gate"], None, 0, gu_out[0]), (*w["up"], None, 0, gu_out[1])],
+                                       exact_codes=True, norm=(nw2, 1e-5))
+            h = silu_mul(g_, u_)
+            forms.add("gate/up grouped + silu_mul")
+        else:
+            forms.add("gate/up pair")
         xh = h if shards == 1 else full_h                   # ... the gathered h
         y = gemv_4bit(xh, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1)[:Hs])
         return y if shards == 1 else x
@@ -631,14 +646,42 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     del sets, g
     torch.cuda.empty_cache()
     ach = nbytes / (us * 1e-6) / 1e9
-    return {"what": "one Llama-3-8B layer's Linear4bit chain: q/k/v+norm grouped, o_proj+residual, gate/up+SiLU+norm "
-                    "pair, down_proj+residual (4 dependent launches), NF4+DQ exact codes, one HIP graph of "
+    name = "Llama-3-70B" if model_name == "llama3-70b" else "Llama-3-8B"
+    return {"what": f"one {name} layer's Linear4bit chain: q/k/v+norm grouped, o_proj+residual, gate/up+SiLU+norm, "
+                    "down_proj+residual, NF4+DQ exact codes, one HIP graph of "
                     f"{layers} layers over {copies} rotating weight sets"
                     + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
-            "shards": shards,
-            "us_per_layer": round(us, 3), "us_per_launch": round(us / 4, 3), "algorithmic_bytes_per_layer": nbytes,
+            "model": model_name, "shards": shards, "gate_up_form": sorted(forms),
+            "us_per_layer": round(us, 3), "algorithmic_bytes_per_layer": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_layer_min": round(min(times), 3), "us_per_layer_max": round(max(times), 3)}
+
+
+def _safe(fn, *a, **k):
+    """fn(*a, **k), or {"error": ...} if it raises: a rank-0 extra measurement never costs the
+    headline line (and never leaves the other ranks waiting in a later collective)."""
+    try:
+        return fn(*a, **k)
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        log(f"bench: {getattr(fn, '__name__', fn)} failed: {type(e).__name__}: {e}")
+        try:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        except Exception:  # noqa: BLE001
+            pass
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def effective_knobs() -> dict:
+    """The measurement knobs in effect: the C launchers' (read once at library load,
+    qz_gemv_knobs) and the Python routing switches (read at import of quantizations_amd.core),
+    with every QZ_* variable set in this process's environment."""
+    from quantizations_amd import _lib, core
+    return {"gemv_launchers": _lib.gemv_knobs(),
+            "routing": {"GEMV_EXACT_CODES": core.GEMV_EXACT_CODES, "PREFILL_GEMM16": core.PREFILL_GEMM16,
+                        "GEMM16_MIN_TILES": core.GEMM16_MIN_TILES,
+                        "PREFILL_FUSED_MAX_T": core._FUSED_MAX_T_ENV},
+            "env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("QZ_")}}
 
 
 def _pmc_traffic(name: str):
@@ -876,6 +919,48 @@ def cpu_baseline(runs: int = 20, warmups: int = 3):
                       f"token (extrapolated, not a decode run)"}
 
 
+def roofline_object(args, layer_ops: str) -> dict:
+    """The line's `roofline` object: the 4096x4096 decode GEMV's launch period (gemv_roofline), its
+    in-kernel duration, the dominant launch of the decode step and the one-launch ceiling."""
+    mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
+    # average launch duration = HIP events around `iters` back-to-back launches on
+    # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
+    # overhead on ROCm and disagrees with rocprofv3, so it is reported only.
+    ach = GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9
+    traffic = _pmc_traffic("gemv_4096_pmc.json")
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_gemv_4bit<Tab,DQ,f16,R=2,WK=1,full-step,CL=%d> 4096x4096 NF4+DQ (LDS byte-table decode, "
+                      "%s codes)" % (int(GEMV_EXTRA.get("codes", "").startswith("exact")), GEMV_EXTRA.get("codes")),
+            "launch_us_avg": round(b2b_us, 3),
+            "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
+            "per_launch_event_us_p10": GEMV_EXTRA.get("per_launch_event_us_p10"),
+            "per_launch_event_us_p90": GEMV_EXTRA.get("per_launch_event_us_p90"),
+            "one_shot_read_floor_us": round(floor_us, 3),
+            "frac_of_one_shot_floor": round(floor_us / b2b_us, 4),
+            # what one launch can reach at all: an empty dependent launch's period
+            # plus the 8.67 MB at peak bandwidth
+            "empty_launch_us": round(empty_us, 3),
+            "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
+                                                                * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
+            "dominant_decode_kernel": _safe(dominant_roofline,
+                prenorm=bool(not args.no_prenorm and not args.no_fuse
+                             and layer_ops in ("all", "norm")),
+                pair=bool(not args.no_mlp_pair and not args.no_fuse and layer_ops in ("all", "all+decoder", "mlp")))}
+    from quantizations_amd import _lib, core
+    ink = _safe(gemv_in_kernel, bool(core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32),
+                                                           torch.float16) & _lib.EXACT_CODES))
+    if ink is not None and "error" in ink:
+        roof["in_kernel"] = ink
+    elif ink is not None:
+        # the kernel's own duration (stamps): what the launch period adds on top is dispatch
+        roof["in_kernel"] = ink
+        roof["in_kernel_us"] = ink["in_kernel_us"]
+        roof["frac_in_kernel"] = round(GEMV_BYTES_4096 / (ink["in_kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    return roof
+
+
 def codes_desc(args, compute_dtype) -> str:
     """The decode GEMV's code table for the bench model (core._gemv_quant_type)."""
     if args.dtype == "bf16":
@@ -908,11 +993,17 @@ def setup_oneshot(rank: int):
     try:
         from quantizations_amd.exchange import OneShotAllGather
         g = OneShotAllGather(slot_bytes=1 << 18)
-        if g.verify():
-            g.warm_graph()   # the process's first captured graph is the slow one (exchange.warm_graph)
-            return g, "oneshot-ipc"
-        log(f"[rank {rank}] one-shot all-gather disagrees with RCCL: using RCCL")
-        return None, "rccl (one-shot failed verification)"
+        if not g.verify():
+            log(f"[rank {rank}] one-shot all-gather disagrees with RCCL: using RCCL")
+            g.close()
+            return None, "rccl (one-shot failed verification)"
+        # the process's first captured graph is the slow one (exchange.warm_graph); its success is
+        # voted over every rank, so either all ranks keep the gatherer or all fall back together
+        if not g.warm_graph():
+            log(f"[rank {rank}] one-shot all-gather failed its warm-up graph on some rank: using RCCL")
+            g.close()
+            return None, "rccl (one-shot failed its warm-up graph)"
+        return g, "oneshot-ipc"
     except Exception as e:  # reported in the line, never fatal to the measurement
         log(f"[rank {rank}] one-shot all-gather unavailable ({type(e).__name__}: {e}): using RCCL")
         return None, f"rccl (one-shot unavailable: {type(e).__name__})"
@@ -1097,7 +1188,7 @@ def main():
         print(json.dumps(dominant_roofline()), flush=True)
         return
     if args.chain_only:
-        print(json.dumps(chain_roofline(shards=args.chain_shards)), flush=True)
+        print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model)), flush=True)
         return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
@@ -1177,42 +1268,9 @@ def main():
     parity = None
     chain = None
     if rank == 0 and not args.no_roofline:
-        mean_us, med_us, b2b_us, floor_us, empty_us = gemv_roofline()
-        # average launch duration = HIP events around `iters` back-to-back launches on
-        # the launch stream / iters; a per-launch event pair adds ~2.3 us of event
-        # overhead on ROCm and disagrees with rocprofv3, so it is reported only.
-        ach = GEMV_BYTES_4096 / (b2b_us * 1e-6) / 1e9
-        traffic = _pmc_traffic("gemv_4096_pmc.json")
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_gemv_4bit<Tab,DQ,f16,R=2,WK=1,full-step,CL=%d> 4096x4096 NF4+DQ (LDS byte-table decode, "
-                          "%s codes)" % (int(GEMV_EXTRA.get("codes", "").startswith("exact")), GEMV_EXTRA.get("codes")),
-                "launch_us_avg": round(b2b_us, 3),
-                "per_launch_event_us_mean": round(mean_us, 3), "per_launch_event_us_median": round(med_us, 3),
-                "per_launch_event_us_p10": GEMV_EXTRA.get("per_launch_event_us_p10"),
-                "per_launch_event_us_p90": GEMV_EXTRA.get("per_launch_event_us_p90"),
-                "one_shot_read_floor_us": round(floor_us, 3),
-                "frac_of_one_shot_floor": round(floor_us / b2b_us, 4),
-                # what one launch can reach at all: an empty dependent launch's period
-                # plus the 8.67 MB at peak bandwidth
-                "empty_launch_us": round(empty_us, 3),
-                "frac_ceiling_one_launch": round(GEMV_BYTES_4096 / ((empty_us + GEMV_BYTES_4096 / (HBM_PEAK_GBS * 1e3))
-                                                                    * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "codes": GEMV_EXTRA.get("codes"), "other_codes_launch_us": GEMV_EXTRA.get("other_codes_launch_us"),
-                "dominant_decode_kernel": dominant_roofline(
-                    prenorm=bool(not args.no_prenorm and not args.no_fuse
-                                 and layer_ops in ("all", "norm")),
-                    pair=bool(not args.no_mlp_pair and not args.no_fuse and layer_ops in ("all", "all+decoder", "mlp")))}
-        from quantizations_amd import _lib, core
-        ink = gemv_in_kernel(bool(core._gemv_quant_type("nf4", core.exact_codes_for(torch.float32), torch.float16)
-                                  & _lib.EXACT_CODES))
-        if ink is not None:
-            # the kernel's own duration (stamps): what the launch period adds on top is dispatch
-            roof["in_kernel"] = ink
-            roof["in_kernel_us"] = ink["in_kernel_us"]
-            roof["frac_in_kernel"] = round(GEMV_BYTES_4096 / (ink["in_kernel_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
-        parity = gemv_parity()
-        chain = chain_roofline()
+        roof = _safe(roofline_object, args, layer_ops)
+        parity = _safe(gemv_parity)
+        chain = _safe(chain_roofline)
 
     layer = None
     if not args.no_roofline:
@@ -1266,6 +1324,7 @@ def main():
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
         line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"
+        line["config"]["knobs"] = _safe(effective_knobs)
         if exchange is not None:
             line["config"]["exchange"] = exchange
         if extra_codes is not None:

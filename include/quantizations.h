@@ -334,6 +334,12 @@ int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, in
                            int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,
                            void *h, void *stream);
 
+/* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
+ * QZ_PAIR_WT, QZ_PAIR_PS: environment variables read ONCE when the library is loaded) and the
+ * device's CU count, as a JSON object written to buf (NUL-terminated when n > the length).
+ * Returns the length of the JSON text.  No reference counterpart (measurement bookkeeping). */
+int qz_gemv_knobs(char *buf, int n);
+
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int qz_version(void);
 

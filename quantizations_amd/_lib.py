@@ -89,6 +89,7 @@ SIGNATURES = {
     "qz_enable_peer_access": [_i],
     "qz_allgather_oneshot": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _p],
     "qz_allgather_oneshot_mode": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _i, _p],
+    "qz_gemv_knobs": [_p, _i],
     "qz_version": [],
 }
 RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll}
@@ -137,3 +138,11 @@ def stream_of(t: torch.Tensor) -> int:
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def gemv_knobs() -> dict:
+    """The decode launchers' measurement knobs as the library read them at load (qz_gemv_knobs)."""
+    import json
+    buf = ctypes.create_string_buffer(512)
+    n = lib.qz_gemv_knobs(buf, len(buf))
+    return json.loads(buf.value.decode()) if 0 < n < len(buf) else {}

@@ -1,6 +1,6 @@
 // diag_stamps.hip -- measurement-only library (libqz_diag.so, NOT the product): the product
 // decode GEMV instantiation with in-kernel timeline stamps (s_memrealtime, 100 MHz chip-wide
-// clock) at wave start and after the wave's last store (gemv.hip, QZ_STAMP / ABL & 512).
+// clock) at wave start and after the wave's last store (gemv.hip, QZ_STAMP / STAMP = 2).
 // bench.py times the kernel's own duration with it -- first wave start to last wave end --
 // which the rocprofv3 tracer cannot resolve at a few microseconds.
 // Built with hidden visibility: only the qz_diag_* entry points are exported, so the
@@ -11,7 +11,7 @@
 #define QZ_DIAG_API extern "C" __attribute__((visibility("default")))
 
 // Stamp buffer: 8 u64 per wave (wave id = block * 4 + wave in block): [0] start, [4] after the
-// wave's stores were issued (the "light" stamps, ABL & 8192: nothing in between is timed, so
+// wave's stores were issued (the "light" stamps, STAMP 2: nothing in between is timed, so
 // the schedule between them is the product's).  Every launch overwrites it.
 QZ_DIAG_API int qz_diag_set_stamp_buffer(unsigned long long *buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_qz_stamp), &buf, sizeof(buf));
@@ -35,11 +35,15 @@ QZ_DIAG_API int qz_diag_gemv_stamped(int M, int K, const void *x, const unsigned
   set_tables(QZ_NF4, nullptr, exact != 0, QZ_DT_F16, &p);
   const unsigned grid = (unsigned)((M + R * 4 - 1) / (R * 4));
   hipStream_t s = (hipStream_t)stream;
-#define QZ_DG(RR, CL_) \
-  hipLaunchKernelGGL((k_gemv_4bit<kModeTab, true, QZ_DT_F16, RR, 1, 4, false, 512 | 8192, true, CL_>), dim3(grid), \
-                     dim3(256), 0, s, p)
-  if (R == 2) { if (exact) QZ_DG(2, true); else QZ_DG(2, false); }
-  else { if (exact) QZ_DG(4, true); else QZ_DG(4, false); }
+  // the product's instantiation for this shape (launch_vec): the straight-line two-step form at
+  // K = 4096, the loop form otherwise; STAMP 2 = start / end stamps only
+  const bool two = two_steps(K, 1, true);
+#define QZ_DG(RR, CL_, TWO_) \
+  hipLaunchKernelGGL((k_gemv_4bit<true, QZ_DT_F16, RR, 1, 4, true, CL_, false, TWO_, 2>), dim3(grid), dim3(256), 0, s, p)
+#define QZ_DG2(RR, CL_) do { if (two) QZ_DG(RR, CL_, true); else QZ_DG(RR, CL_, false); } while (0)
+  if (R == 2) { if (exact) QZ_DG2(2, true); else QZ_DG2(2, false); }
+  else { if (exact) QZ_DG2(4, true); else QZ_DG2(4, false); }
+#undef QZ_DG2
 #undef QZ_DG
   QZ_LAUNCH_CHECK();
   *nwaves = (int)grid * 4;

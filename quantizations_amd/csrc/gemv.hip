@@ -13,75 +13,57 @@
 // elements; lane l of a wave owns bytes [16 l, 16 l + 16) of the step, i.e.
 // 32 consecutive elements that always sit inside one scale block.  A wave
 // handles R rows of one step at a time, so its 64 B slice of x (fp16) is
-// loaded once and reused R times; the 4 waves of a 256-thread workgroup are
-// split WK ways along K (steps s = wk, wk+WK, ...) and RG = 4/WK ways along
-// rows, and the WK partial sums meet in LDS.  Weight loads are 16 B/lane
-// (1 KiB per wave instruction, fully coalesced) and non-temporal: each byte
-// is read exactly once per call.
+// loaded once and reused R times; the NW waves of a workgroup are split WK
+// ways along K (steps s = wk, wk+WK, ...) and RG = NW/WK ways along rows, and
+// the WK partial sums meet in LDS.  Weight loads are 16 B/lane (1 KiB per wave
+// instruction, fully coalesced) and non-temporal: each byte is read exactly
+// once per call.
 //
-// Nibble decode (production: kModeTab).  A workgroup first writes a 256-entry
-// table to LDS: entry b = the two fp16 codes of packed byte b, i.e. exactly
-// the half2 operand that v_dot2 multiplies with the natural-order x pair.
-// Decoding a byte is then one address computation (2 VALU) and one
-// ds_read_b32; the table is stored 32 times, copy j wholly inside bank j, and
-// lane l reads copy l % 32, so the random byte values never conflict.  Any
-// 16-entry codebook works (NF4, FP4 x12 with the sign in bit 3, a runtime LUT).
-// The older register-only decodes are kept for the microbenchmarks:
-//  * kModeFP4: the 8 FP4 magnitudes x12 have zero low bytes, so one v_perm
-//    per 4 nibbles yields the fp16 high bytes and the sign bit is OR-ed in.
-//  * kModeLUT16: two 8-entry v_perm lookups per fp16 byte plane, AND-combined
-//    on bit 3, then pairs (e0,e2),(e4,e6),(e1,e3),(e5,e7).  ~3.5 VALU ops per
-//    weight, half of them half-rate v_perm: VALU-issue-bound on gfx950.
-// Products: v_dot2_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
+// Nibble decode: a workgroup first writes a 256-entry table to LDS: entry b =
+// the two codes of packed byte b, i.e. exactly the operand pair that v_dot2
+// multiplies with the natural-order x pair.  Decoding a byte is then one
+// address computation and one LDS read; the table is stored in bank-private
+// copies (lane l reads its own copy), so the random byte values never conflict.
+// Any 16-entry codebook works (NF4, FP4 x12 with the sign in bit 3, a runtime LUT).
+// Products: v_dot2c_f32_f16 (fp16 x fp16 exact products, fp32 accumulate);
 // per 32-element chunk the fp32 dot is scaled by the block absmax with one
-// FMA.  On the product byte-table path bf16 x is dotted RAW against bf16 hi + lo
-// code pairs (v_dot2c_f32_bf16, kRawBF) and fp32 x RAW against fp32 codes
-// (v_fma_f32, kRawF32): no conversion of x.  Only the register-decode modes
-// (microbenchmarks) still split fp32/bf16 x into hi+lo fp16 halves after a
-// per-lane power-of-two pre-scale that puts the chunk's largest |x| in
-// [2^14, 2^15) (kScaled; undone exactly on the fp32 dot).
-// Exact codes (CL): a runtime codebook (`lut`, the reference ABI's fp32
-// quant_map, kernels.cu:1115-1120) is NOT rounded to fp16: each code c is
-// stored as c * 2^S = ch + cl, two fp16 values (~2^-23 relative: fp32-class),
-// in a 64-bit table entry (hi pair, lo pair) read with one ds_read_b64, and
-// the dot takes ch*x + cl*x.  S (power of two, from max|code|) is undone on
-// the output.
+// FMA.  bf16 x is dotted RAW against bf16 hi + lo code pairs (v_dot2c_f32_bf16)
+// and fp32 x RAW against fp32 codes (v_fma_f32): no conversion of x.
+// Exact codes (CL, fp16 x): each code c is stored as c * 2^S = ch + cl, two fp16
+// values (~2^-23 relative: fp32-class), in a 64-bit table entry (hi pair, lo
+// pair) read with one ds_read_b64, and the dot takes ch*x + cl*x.  S (power of
+// two, from max|code|) is undone on the output.
+//
+// The variants this file once carried for measurement only (register v_perm
+// decodes, MFMA tile / diagonal decodes, the streaming form, step rings, the
+// next-launch prefetch, fp32-code FMA forms, ablation bits) lost on every decode
+// shape and were removed in round 5; DESIGN.md section 4.1 / 11 keeps their numbers
+// and the git history their code.
 #include "common.h"
 
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
-#include <utility>
+#include <cstring>
 
 namespace qz {
 
-enum {
-  kModeFP4 = 0,    // sign/magnitude FP4: 8-entry x12 table in VALU
-  kModeLUT16 = 1,  // any 16-entry codebook (NF4): AND-combined v_perm lookups in VALU
-  kModeRaw = 2,    // benchmark-only: no decode
-  kModeTab = 3     // any 16-entry codebook: byte -> half2 table in LDS, bank-private copies
-};
-
-// kModeTab: one LDS entry per packed BYTE value holds the two decoded fp16
-// codes (element 2m in the low half, 2m+1 in the high half) -- exactly the
-// operand of v_dot2 against the natural-order x pair, so the decode is one
-// address computation + one ds_read_b32 per two weights and NO v_perm.  A
-// ds_read_b32 serves each 32-lane half of the wave in one LDS cycle when its
-// lanes hit distinct banks (MI355X_MICROARCH.md, LDS table); byte values are
-// random, so the table is stored 32 times, copy j entirely in bank j
-// (dword e*32 + j), and lane l reads copy l % 32: never a bank conflict.
+// Bank-private table copies: 32 copies of a 4-B entry (fp16 codes) or 16 copies
+// of an 8-B entry (exact / bf16 / fp32 codes) -- 128 B per byte value, 32 KiB.
+// A ds_read_b32 serves each 32-lane half of the wave in one LDS cycle when its
+// lanes hit distinct banks (MI355X_MICROARCH.md, LDS table): copy j lives wholly in
+// bank j (dword e*32 + j) and lane l reads copy l % 32.  With 8-B entries a
+// 32-lane group holds two lanes per copy, which collide only when their byte
+// values have the same parity (1.5-way on average).  WT ("wide table"): 256 B per
+// byte value (64 / 32 copies), 64 KiB, every copy bank-private, and the lookup
+// address is one v_perm.
 constexpr int kTabCopies = 32;
 constexpr int kTabDwords = 256 * kTabCopies;  // 32 KiB
-// CL (exact codes): 64-bit entries (hi pair, lo pair), 16 copies -> the same
-// 128 B per byte value and 32 KiB, so the byte -> address computation and the
-// occupancy are unchanged.  Lane l reads copy l % 16: a ds_read_b64 lane group
-// (32 lanes, bank = dword mod 64) then holds two lanes per copy, which collide
-// only when their byte values have the same parity (entry stride 32 dwords):
-// 1.5-way on average.
 constexpr int kTabCopiesCL = 16;
 
-// The byte tables of the two built-in codebooks, computed at compile time and
-// stored once in device memory with each entry repeated 4 times (one 16-B
-// store per 4 bank copies): a workgroup fills its LDS image with 8 plain
-// 16-B copies per thread instead of decoding 256 entries.
+// The byte tables of the built-in codebooks, computed at compile time and stored
+// once in device memory with each entry repeated 4 times (one 16-B store covers
+// 4 bank copies): a workgroup fills its LDS image with plain 16-B copies.
 constexpr uint16_t f16_bits_rne_c(float f) {  // normal-range values and +-0 only
   const uint32_t u = __builtin_bit_cast(uint32_t, f);
   const uint32_t sign = (u >> 16) & 0x8000u, au = u & 0x7FFFFFFFu;
@@ -101,6 +83,7 @@ constexpr ByteTable make_byte_table(const uint16_t (&c)[16]) {
     for (int k = 0; k < 4; ++k) t.v[4 * e + k] = (uint32_t)c[e >> 4] | ((uint32_t)c[e & 15] << 16);
   return t;
 }
+// NF4 codebook q_data (reference kernels.cu:851)
 constexpr float kNF4Host[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
                                 -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
                                 0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
@@ -140,9 +123,9 @@ constexpr ByteTable make_nf4_exact_table() {
   }
   return t;
 }
-// bf16 activations (round 2): the codes as bf16 hi + lo pairs -- c = hi + lo to ~2^-16 --
-// dotted straight against the raw bf16 x pairs with v_dot2c_f32_bf16 (no x conversion, no
-// pre-scale: bf16 has fp32's exponent range).  Entries {hi pair, lo pair}, the CL geometry.
+// bf16 activations: the codes as bf16 hi + lo pairs -- c = hi + lo to ~2^-16 -- dotted straight
+// against the raw bf16 x pairs with v_dot2c_f32_bf16 (bf16 has fp32's exponent range: no
+// pre-scale).  Entries {hi pair, lo pair}, the CL geometry.
 constexpr uint16_t bf16_bits_rne_c(float f) {  // finite values
   const uint32_t u = __builtin_bit_cast(uint32_t, f);
   return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
@@ -165,12 +148,8 @@ constexpr ByteTable make_bf16_table(const float (&c)[16]) {
 // FP4 x12 magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3} are exact in bf16 (lo = 0); out_scale 1/12
 constexpr float kFP4x12Host[16] = {0.0f, 0.0625f, 8.0f, 12.0f, 4.0f, 6.0f, 2.0f, 3.0f,
                                    -0.0f, -0.0625f, -8.0f, -12.0f, -4.0f, -6.0f, -2.0f, -3.0f};
-__device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
-__device__ const ByteTable g_byte_tab_nf4x = make_nf4_exact_table();
-__device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
-__device__ const ByteTable g_byte_tab_nf4_bf = make_bf16_table(kNF4Host);
-// fp32 activations (round 2): entries {code[e >> 4], code[e & 15]} as fp32 -- the reference's
-// own fp32 quant_map values (kernels.cu:1115-1120) -- multiplied into the raw fp32 x by v_fma_f32
+// fp32 activations: entries {code[e >> 4], code[e & 15]} as fp32 -- the reference's own fp32
+// quant_map values (kernels.cu:1115-1120) -- multiplied into the raw fp32 x by v_fma_f32
 constexpr ByteTable make_f32_table(const float (&c)[16]) {
   ByteTable t{};
   for (int e = 0; e < 256; ++e) {
@@ -179,6 +158,10 @@ constexpr ByteTable make_f32_table(const float (&c)[16]) {
   }
   return t;
 }
+__device__ const ByteTable g_byte_tab_nf4 = make_nf4_table();
+__device__ const ByteTable g_byte_tab_nf4x = make_nf4_exact_table();
+__device__ const ByteTable g_byte_tab_fp4 = make_byte_table(kFP4x12Bits);
+__device__ const ByteTable g_byte_tab_nf4_bf = make_bf16_table(kNF4Host);
 __device__ const ByteTable g_byte_tab_fp4_bf = make_bf16_table(kFP4x12Host);
 __device__ const ByteTable g_byte_tab_nf4_f32 = make_f32_table(kNF4Host);
 __device__ const ByteTable g_byte_tab_fp4_f32 = make_f32_table(kFP4x12Host);
@@ -218,29 +201,16 @@ struct GemvParams {
   ScaleSrc sc;
   const void *bias;
   void *y;
-  const float *lut;  // runtime 16-entry codebook (kModeLUT16) or nullptr
+  const float *lut;  // runtime 16-entry codebook (always decoded exactly) or nullptr
   long long block_base;
   int M, K;
   int bs_log2, bs2_log2;
   float out_scale;
-  int tabsel;        // kModeTab: 0 = NF4, 1 = FP4 (x12), 2 = exact NF4 (CL) precomputed byte table;
-                     // lut != nullptr builds an exact (CL) table in kernel
-  uint32_t tab[8];
-  uint32_t tab_lo[8];  // exact codes (CL): fp16 byte planes of the lo parts (the hi parts are tab)
+  int tabsel;        // built-in byte table: 0 = NF4, 1 = FP4 (x12), 2 = exact NF4 (CL)
   const void *nw;    // fused pre-norm (NRM): the RMSNorm weight [K], or nullptr
   float eps;         //   and its epsilon
   const void *res;   // residual [M] added after the output rounding (y = round(round(x W^T) + res)), or nullptr
-  // prefetch (PF): the first pf_chunks KiB of each of pf_rows rows (stride pf_row_bytes) of the NEXT
-  // launch's packed weight, read into the caches (Infinity Cache) once this launch's own loads are out
-  const unsigned char *pf;
-  uint32_t pf_row_bytes;
-  int pf_rows, pf_chunks;
 };
-
-__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
-  return __builtin_amdgcn_perm(s0, s1, sel);
-}
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, a), __builtin_bit_cast(h2_t, b), c, false);
@@ -249,7 +219,7 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 // Kernel arguments are read ONCE at entry and laundered through an empty asm:
 // the compiler then keeps them in SGPRs instead of re-fetching them from the
 // kernarg segment at each use (every re-fetch is a serialized scalar-cache miss
-// on the critical path of a ~µs kernel).
+// on the critical path of a ~us kernel).
 template <typename T> __device__ __forceinline__ T keep_s(T v) {
   asm volatile("" : "+s"(v));
   return v;
@@ -264,18 +234,17 @@ template <typename T> __device__ __forceinline__ T *keep_sp(T *v) {
   return (T *)g;
 }
 
-// Diagnostic timeline stamps (dev builds only: scripts/microbench defines
-// QZ_STAMPS and instantiates ABL & 512).  The product library compiles none of
-// this.  Per wave: s_memrealtime (100 MHz, chip-wide) at fixed points, stored
-// once at the end by lane 0 with the wave's XCC / HW ids.
+// Diagnostic timeline stamps (measurement-only builds: diag_stamps.hip and scripts/microbench
+// define QZ_STAMPS and instantiate STAMP != 0).  The product library compiles none of this.  Per
+// wave: s_memrealtime (100 MHz, chip-wide) at fixed points, stored once at the end by lane 0 with
+// the wave's XCC / HW ids.  STAMP 1: all points; STAMP 2 ("light"): only the start (0) and end
+// (4) stamps, so the schedule between them is the product's (bench.py's in-kernel time).
 #ifdef QZ_STAMPS
 __device__ unsigned long long *g_qz_stamp;
 #define QZ_STAMP_DECL unsigned long long qz_st_[6] = {0, 0, 0, 0, 0, 0}
-// ABL & 8192 ("light"): only the start (0) and end (4) stamps, flushed as two stores, so the
-// instrumentation leaves the kernel's schedule between them untouched (bench.py's in-kernel time)
 #define QZ_STAMP(k)                                                                  \
   do {                                                                               \
-    if constexpr ((ABL & 512) != 0 && ((ABL & 8192) == 0 || (k) == 0 || (k) == 4)) { \
+    if constexpr (STAMP != 0 && (STAMP == 1 || (k) == 0 || (k) == 4)) {              \
       __builtin_amdgcn_sched_barrier(0);                                             \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(qz_st_[k])::"memory"); \
       __builtin_amdgcn_sched_barrier(0);                                             \
@@ -283,13 +252,13 @@ __device__ unsigned long long *g_qz_stamp;
   } while (0)
 #define QZ_STAMP_FLUSH(wave_id)                                                      \
   do {                                                                               \
-    if constexpr ((ABL & 512) != 0) {                                                \
+    if constexpr (STAMP != 0) {                                                      \
       uint32_t xcc, hw;                                                              \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));             \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));               \
       qz_st_[5] = ((unsigned long long)xcc << 32) | hw;                              \
       if ((threadIdx.x & 63) == 0) {                                                 \
-        if constexpr ((ABL & 8192) != 0) {                                           \
+        if constexpr (STAMP == 2) {                                                  \
           g_qz_stamp[(size_t)(wave_id) * 8 + 0] = qz_st_[0];                         \
           g_qz_stamp[(size_t)(wave_id) * 8 + 4] = qz_st_[4];                         \
         } else {                                                                     \
@@ -325,204 +294,24 @@ __device__ __forceinline__ GemvParams load_params(const GemvParams &in) {
   p.out_scale = keep_s(in.out_scale);
   p.tabsel = keep_s(in.tabsel);
   p.res = keep_sp(in.res);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) p.tab[i] = keep_s(in.tab[i]);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) p.tab_lo[i] = keep_s(in.tab_lo[i]);
   p.nw = keep_sp(in.nw);
   p.eps = keep_s(in.eps);
-  p.pf = keep_sp(in.pf);
-  p.pf_row_bytes = keep_s(in.pf_row_bytes);
-  p.pf_rows = keep_s(in.pf_rows);
-  p.pf_chunks = keep_s(in.pf_chunks);
   return p;
 }
 
-// FP4: 8 nibbles -> 4 half2 in natural order P[j] = (e_2j, e_2j+1), values x12.
-__device__ __forceinline__ void decode_fp4(uint32_t w, uint32_t t0, uint32_t t1, uint32_t (&P)[4]) {
-  const uint32_t hh = perm(t1, t0, (w >> 4) & 0x07070707u) | (w & 0x80808080u);
-  const uint32_t hl = perm(t1, t0, w & 0x07070707u) | ((w << 4) & 0x80808080u);
-  P[0] = perm(hh, hl, 0x000C040Cu);
-  P[1] = perm(hh, hl, 0x010C050Cu);
-  P[2] = perm(hh, hl, 0x020C060Cu);
-  P[3] = perm(hh, hl, 0x030C070Cu);
-}
-
-// 16-entry codebook: 8 nibbles -> (e0,e2),(e4,e6),(e1,e3),(e5,e7).
-// Each fp16 byte plane is a 16-entry lookup done as two 8-entry v_perm
-// lookups AND-ed together: the selector byte is the nibble with its bit 3
-// copied to bit 7, so entries 0-7 index the first table directly and
-// entries 8-15 give a selector >= 0x88, which v_perm maps to 0xFF; XOR 0x88
-// swaps the roles for the second table.  (v_perm, v_bfi and v_dot2c issue at
-// half rate on gfx950; this form needs no mask perm and no v_bfi.)
-__device__ __forceinline__ void decode_lut16(uint32_t w, const uint32_t (&t)[8], uint32_t (&P)[4]) {
-  uint32_t ah = ((w >> 4) & 0x0F0F0F0Fu) | (w & 0x80808080u);   // high nibbles (even elements)
-  asm("" : "+v"(ah));  // keep the XOR below a full-rate v_xor (not a re-associated v_bitop3)
-  const uint32_t bh = ah ^ 0x88888888u;
-  const uint32_t lh = perm(t[1], t[0], ah) & perm(t[3], t[2], bh);
-  const uint32_t hh = perm(t[5], t[4], ah) & perm(t[7], t[6], bh);
-  uint32_t al = (w & 0x0F0F0F0Fu) | ((w << 4) & 0x80808080u);   // low nibbles (odd elements)
-  asm("" : "+v"(al));
-  const uint32_t bl = al ^ 0x88888888u;
-  const uint32_t ll = perm(t[1], t[0], al) & perm(t[3], t[2], bl);
-  const uint32_t hl = perm(t[5], t[4], al) & perm(t[7], t[6], bl);
-  P[0] = perm(hh, lh, 0x05010400u);
-  P[1] = perm(hh, lh, 0x07030602u);
-  P[2] = perm(hl, ll, 0x05010400u);
-  P[3] = perm(hl, ll, 0x07030602u);
-}
-
-// x slice of one lane for one step: 32 activations, loaded raw (so that the
-// loads retire in issue order without forcing early waits) and turned into
-// 16 half2 "hi" (+ "lo" for fp32/bf16 activations) in the pair order of MODE
-// only at compute time.
-template <int MODE, int DT> struct XSlice {
-  // fp32 x needs the lo part; a bf16 value (8-bit significand) pre-scaled into fp16's range is
-  // exact in the hi part, and whatever it loses below fp16's smallest subnormal its lo part
-  // (rtz of a residual < 2^-24) loses too: bf16 lo is identically zero, so it is not formed
-  // the byte-table decode takes bf16 x raw against bf16 code pairs (kRawBF) and fp32 x raw
-  // against fp32 codes (kRawF32): no conversion at all
-  static constexpr bool kRawBF = DT == QZ_DT_BF16 && MODE == kModeTab;
-  static constexpr bool kRawF32 = DT == QZ_DT_F32 && MODE == kModeTab;
-  static constexpr bool kSplit = DT == QZ_DT_F32 && !kRawF32;
-  static constexpr bool kScaled = DT != QZ_DT_F16 && !kRawBF && !kRawF32;
-  static constexpr int kWords = DT == QZ_DT_F32 ? 32 : 16;  // raw dwords per lane
-  uint32_t raw[kWords];
-
-  __device__ __forceinline__ void load(const void *x, uint32_t e0) {
-    const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(x) +
-                                                     e0 * (DT == QZ_DT_F32 ? 4u : 2u));
-#pragma unroll
-    for (int i = 0; i < kWords / 4; ++i) {
-      const u32x4 v = p[i];
-      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
-    }
-  }
-
-  __device__ __forceinline__ void load_lds(const unsigned char *lds_x, int e0) {
-    const u32x4 *p = reinterpret_cast<const u32x4 *>(lds_x + e0 * (DT == QZ_DT_F32 ? 4 : 2));
-#pragma unroll
-    for (int i = 0; i < kWords / 4; ++i) {
-      const u32x4 v = p[i];
-      raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
-    }
-  }
-
-  // hi/lo half2 operands, pair order of MODE.  fp32/bf16: the chunk is first
-  // scaled by 2^se so that its largest |x| lies in [2^14, 2^15) (hi = rtz
-  // never saturates, lo never flushes); usc = 2^-se undoes it on the dot.
-  __device__ __forceinline__ void prepare(uint32_t (&hi)[16], uint32_t (&lo)[kSplit ? 16 : 1], float &usc) const {
-    usc = 1.0f;
-    if constexpr (kRawF32) {
-      return;  // chunk_dot_tab_f32 reads raw[] itself
-    } else if constexpr (kRawBF) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) hi[i] = raw[i];
-    } else if constexpr (DT == QZ_DT_F16) {
-      if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) hi[i] = raw[i];
-      } else {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {  // per 8 elements: (x0,x2),(x4,x6),(x1,x3),(x5,x7)
-          hi[4 * d + 0] = perm(raw[4 * d + 1], raw[4 * d + 0], 0x05040100u);
-          hi[4 * d + 1] = perm(raw[4 * d + 3], raw[4 * d + 2], 0x05040100u);
-          hi[4 * d + 2] = perm(raw[4 * d + 1], raw[4 * d + 0], 0x07060302u);
-          hi[4 * d + 3] = perm(raw[4 * d + 3], raw[4 * d + 2], 0x07060302u);
-        }
-      }
-    } else {
-      float f[32];
-      if constexpr (DT == QZ_DT_F32) {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) f[i] = __uint_as_float(raw[i]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          f[2 * i] = __uint_as_float(raw[i] << 16);
-          f[2 * i + 1] = __uint_as_float(raw[i] & 0xFFFF0000u);
-        }
-      }
-      // chunk max |x| (v_max3_f32 with abs modifiers; NaN is ignored here and
-      // still propagates through the dot), its biased exponent E, se = 141 - E
-      float mx = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 32; i += 2) mx = fmaxf(mx, fmaxf(fabsf(f[i]), fabsf(f[i + 1])));
-      const int E = (int)(__float_as_uint(mx) >> 23);
-      const int se = min(141 - E, 100);                    // in [-114, 100]: both scales are normal
-      const float sc = __uint_as_float((uint32_t)(127 + se) << 23);
-      usc = __uint_as_float((uint32_t)(127 - se) << 23);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        int a[4], b[4];
-        if constexpr (MODE == kModeFP4 || MODE == kModeTab) {
-          a[0] = 0; b[0] = 1; a[1] = 2; b[1] = 3; a[2] = 4; b[2] = 5; a[3] = 6; b[3] = 7;
-        } else {
-          a[0] = 0; b[0] = 2; a[1] = 4; b[1] = 6; a[2] = 1; b[2] = 3; a[3] = 5; b[3] = 7;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          // hi = rtz(f s) (|f s| < 2^15), lo = rtz(f s - hi); f s - hi is exact
-          const float fa = f[8 * d + a[j]] * sc, fb = f[8 * d + b[j]] * sc;
-          const auto h = __builtin_amdgcn_cvt_pkrtz(fa, fb);
-          hi[4 * d + j] = __builtin_bit_cast(uint32_t, h);
-          if constexpr (kSplit) {
-            const float ra = fa - (float)h.x, rb = fb - (float)h.y;
-            lo[4 * d + j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(ra, rb));
-          }
-        }
-      }
-    }
-  }
-};
-
-// dot of one lane's 16-byte weight chunk (32 codes) with its x slice
-template <int MODE, bool SPLIT>
-__device__ __forceinline__ float chunk_dot(const u32x4 &wv, const uint32_t (&hi)[16],
-                                           const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t (&t)[8]) {
-  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
-  float s0 = 0.0f, s1 = 0.0f;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    uint32_t P[4];
-    if constexpr (MODE == kModeFP4) {
-      decode_fp4(w[d], t[0], t[1], P);
-    } else if constexpr (MODE == kModeLUT16) {
-      decode_lut16(w[d], t, P);
-    } else {
-      P[0] = w[d]; P[1] = w[d] ^ 1u; P[2] = w[d] ^ 2u; P[3] = w[d] ^ 3u;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j & 1) s1 = dot2(P[j], hi[4 * d + j], s1);
-      else s0 = dot2(P[j], hi[4 * d + j], s0);
-      if constexpr (SPLIT) {
-        if (j & 1) s1 = dot2(P[j], lo[4 * d + j], s1);
-        else s0 = dot2(P[j], lo[4 * d + j], s0);
-      }
-    }
-  }
-  return s0 + s1;
-}
-
-// kModeTab: dot of one lane's 16-byte chunk through the LDS byte table.
-// `jb` selects the lane's bank-private copy: 4 * (lane % 32), or for CL
-// (64-bit exact-code entries) 8 * (lane % 16).  Both tables use 128 B per
-// byte value, so the address of byte m is (byte << 7) | jb either way.
-// (ABL: benchmark-only ablations -- 16 replaces the dot products by integer
-// adds, 32 replaces the table reads by the addresses themselves.)
-template <bool SPLIT, int ABL = 0, bool CL = false, bool WT = false, bool BF = false>
-__device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&hi)[16],
-                                               const uint32_t (&lo)[SPLIT ? 16 : 1], const uint32_t *s_tab,
+// Dot of one lane's 16-byte weight chunk (32 codes) with its x slice through the LDS byte
+// table.  `jb` selects the lane's bank-private copy; the address of byte m is
+// (byte << 7) | jb (WT: one v_perm builds (byte << 8) | jb).  W (wide entries: CL / bf16):
+// each entry holds a {hi pair, lo pair} and the dot adds lo x x.
+template <bool W, bool WT = false, bool BF = false>
+__device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (&xh)[16], const uint32_t *s_tab,
                                                uint32_t jb) {
-  static_assert(!BF || CL, "bf16 entries use the 64-bit (CL) table geometry");
+  static_assert(!BF || W, "bf16 entries use the 64-bit table geometry");
   const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
   const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  uint32_t v[16], vl[CL ? 16 : 1];
+  uint32_t v[16], vl[W ? 16 : 1];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    // byte m of w, times the stride of one entry (128 B; WT: 256 B), plus the copy.  WT builds
-    // the address with ONE v_perm: byte 0 = the lane's copy offset jb (< 256), byte 1 = byte m
     uint32_t a[4];
     if constexpr (WT) {
 #pragma unroll
@@ -535,10 +324,7 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      if constexpr ((ABL & 32) != 0) {
-        v[4 * d + m] = a[m];
-        if constexpr (CL) vl[4 * d + m] = a[m] ^ 1u;
-      } else if constexpr (CL) {
+      if constexpr (W) {
         const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a[m]);
         v[4 * d + m] = e.x;
         vl[4 * d + m] = e.y;
@@ -547,35 +333,25 @@ __device__ __forceinline__ float chunk_dot_tab(const u32x4 &wv, const uint32_t (
       }
     }
   }
-  if constexpr ((ABL & 16) != 0) {
-    uint32_t u0 = 0, u1 = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i & 1) u1 += v[i] ^ hi[i];
-      else u0 += v[i] ^ hi[i];
-    }
-    return (float)(u0 + u1);
-  }
   float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     float &acc = (i & 1) ? s1 : s0;
     if constexpr (BF) {  // bf16 code pairs (hi, lo) against the raw bf16 x pair
-      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, v[i]), __builtin_bit_cast(bf16x2_t, hi[i]),
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, v[i]), __builtin_bit_cast(bf16x2_t, xh[i]),
                                             acc, false);
-      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, vl[i]), __builtin_bit_cast(bf16x2_t, hi[i]),
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, vl[i]), __builtin_bit_cast(bf16x2_t, xh[i]),
                                             acc, false);
       continue;
     }
-    acc = dot2(v[i], hi[i], acc);
-    if constexpr (CL) acc = dot2(vl[i], hi[i], acc);   // code residual x x_hi
-    if constexpr (SPLIT) acc = dot2(v[i], lo[i], acc);  // code_hi x x residual
+    acc = dot2(v[i], xh[i], acc);
+    if constexpr (W) acc = dot2(vl[i], xh[i], acc);   // code residual x x
   }
   return s0 + s1;
 }
 
-// fp32 x (kRawF32): byte m of the lane's chunk holds elements 2m (high nibble) and 2m + 1;
-// its 64-bit entry {code_hi, code_lo} (fp32) goes into two v_fma_f32 with the raw x.  Same
+// fp32 x: byte m of the lane's chunk holds elements 2m (high nibble) and 2m + 1; its 64-bit
+// entry {code_hi, code_lo} (fp32) goes into two v_fma_f32 with the raw x.  Same
 // 128-B-per-byte-value geometry as the CL table.
 __device__ __forceinline__ float chunk_dot_tab_f32(const u32x4 &wv, const uint32_t (&xr)[32], const uint32_t *s_tab,
                                                    uint32_t jb) {
@@ -598,101 +374,6 @@ __device__ __forceinline__ float chunk_dot_tab_f32(const u32x4 &wv, const uint32
   return s0 + s1;
 }
 
-// Exact codes by mixed-precision FMA (FM, round 4): the byte table holds the two codes as fp32
-// (the kRawF32 table: the reference's fp32 quant_map values, kernels.cu:1115-1120) and each
-// goes into one v_fma_mix_f32 with its raw fp16 activation, the half picked by op_sel -- no x
-// conversion, no hi/lo code split.  Per packed byte: one ds_read_b64 and two full-rate FMAs
-// (the hi + lo table needs two half-rate v_dot2c).  The products are fp32 (an fp16 x an fp32
-// code, rounded once), as the reference's fp32 FMA chain (kernels.cu:1169-1210).
-// Addresses: AD = 0 builds (byte << 7) | jb with two VALU (the 16-copy, 128-B-entry table);
-// AD = 1 is the 256-B-entry table (WT: 32 bank-private copies, no conflicts) addressed by ONE
-// v_mov_b32_sdwa that writes the byte into bits 8..15 of a register whose byte 0 holds the
-// lane's copy offset jb for the whole kernel (`ad`, initialised once; bytes 2-3 stay zero).
-template <int M_> __device__ __forceinline__ void sdwa_byte1(uint32_t &a, uint32_t w) {
-  if constexpr (M_ == 0) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(a) : "v"(w));
-  else if constexpr (M_ == 1) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(a) : "v"(w));
-  else if constexpr (M_ == 2) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(w));
-  else asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(a) : "v"(w));
-}
-template <int AD>
-__device__ __forceinline__ float chunk_dot_tab_fm(const u32x4 &wv, const uint32_t (&xr)[16], const uint32_t *s_tab,
-                                                  uint32_t jb, uint32_t (&ad)[16]) {
-  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
-  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    uint32_t a[4];
-    if constexpr (AD == 1) {
-      sdwa_byte1<0>(ad[4 * d + 0], w[d]);
-      sdwa_byte1<1>(ad[4 * d + 1], w[d]);
-      sdwa_byte1<2>(ad[4 * d + 2], w[d]);
-      sdwa_byte1<3>(ad[4 * d + 3], w[d]);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = ad[4 * d + m];
-    } else {
-      a[0] = ((w[d] << 7) & 0x7F80u) | jb;
-      a[1] = ((w[d] >> 1) & 0x7F80u) | jb;
-      a[2] = ((w[d] >> 9) & 0x7F80u) | jb;
-      a[3] = ((w[d] >> 17) & 0x7F80u) | jb;
-    }
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a[m]);
-      const uint32_t xv = xr[4 * d + m];   // x[2j] in the low half, x[2j + 1] in the high half
-      // written out: left to itself hipcc SLP-packs the scalar FMAs into v_pk_fma_f32 fed by
-      // v_cvt_f32_f16 + v_mov copies (twice the VALU)
-      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(s[(2 * m) & 3]) : "v"(xv), "v"(e.x));
-      asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(s[(2 * m + 1) & 3]) : "v"(xv), "v"(e.y));
-    }
-  }
-  return (s[0] + s[1]) + (s[2] + s[3]);
-}
-
-// Exact codes against fp32 x (XF, round 4): the fp16 x of a step is widened to fp32 once (shared by
-// the wave's R rows) and each packed byte's fp32 code pair {code(hi nibble), code(lo nibble)} (the
-// kRawF32 table) meets its x pair in full-rate fp32 FMAs: PK = 0 two v_fma_f32, PK = 1 one
-// v_pk_fma_f32.  The products are fp32 (exact code x exact x, rounded once), as the reference's fp32
-// FMA chain (kernels.cu:1169-1210).
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-template <int PK>
-__device__ __forceinline__ float chunk_dot_tab_xf(const u32x4 &wv, const f32x2_t (&xf)[16], const uint32_t *s_tab,
-                                                  uint32_t jb) {
-  const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
-  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  f32x2_t s2[2] = {f32x2_t{0.0f, 0.0f}, f32x2_t{0.0f, 0.0f}};
-  float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t a[4] = {((w[d] << 7) & 0x7F80u) | jb, ((w[d] >> 1) & 0x7F80u) | jb,
-                           ((w[d] >> 9) & 0x7F80u) | jb, ((w[d] >> 17) & 0x7F80u) | jb};
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const f32x2_t e = *reinterpret_cast<const f32x2_t *>(tb + a[m]);
-      if constexpr (PK) {
-        asm("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(s2[m & 1]) : "v"(e), "v"(xf[4 * d + m]));
-      } else {
-        // written out: hipcc would SLP-pack the pair into v_pk_fma_f32 (+ register copies), which
-        // issues no faster than the two full-rate FMAs it replaces
-        const float ex = e.x, ey = e.y, xx = xf[4 * d + m].x, xy = xf[4 * d + m].y;
-        asm("v_fmac_f32 %0, %1, %2" : "+v"(s[(2 * m) & 3]) : "v"(ex), "v"(xx));
-        asm("v_fmac_f32 %0, %1, %2" : "+v"(s[(2 * m + 1) & 3]) : "v"(ey), "v"(xy));
-      }
-    }
-  }
-  if constexpr (PK) return (s2[0].x + s2[1].x) + (s2[0].y + s2[1].y);
-  return (s[0] + s[1]) + (s[2] + s[3]);
-}
-
-// compile-time loop: f(std::integral_constant<int, 0>{}) .. f(<N - 1>)
-template <typename F, int... Ns>
-__device__ __forceinline__ void gv_static_for_impl(F &&f, std::integer_sequence<int, Ns...>) {
-  (f(std::integral_constant<int, Ns>{}), ...);
-}
-template <int N, typename F> __device__ __forceinline__ void gv_static_for(F &&f) {
-  gv_static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
 // Sum over the 64 lanes, result valid in lane 63 only: an inclusive row scan
 // (row_shr 1, 2, 4, 8) then row_bcast:15 / row_bcast:31 -- six DPP adds, no
 // readlane round trips through SGPRs.
@@ -709,28 +390,9 @@ __device__ __forceinline__ float wave_sum_last(float v) {
   return v;
 }
 
-// Builds the kModeTab byte table from the 16-entry fp16 byte planes t[8]
-// (every thread of the workgroup takes part; the caller synchronises).
-template <int NT, int PIECES = kTabCopies / 4>
-__device__ __forceinline__ void build_byte_table(uint32_t *s_tab, const uint32_t (&t)[8]) {
-  for (int e = threadIdx.x; e < 256; e += NT) {
-    uint32_t P[4];
-    decode_lut16((uint32_t)e, t, P);  // byte 0 = e: P[0].lo = code[e >> 4], P[2].lo = code[e & 15]
-    const uint32_t v = (P[0] & 0xFFFFu) | (P[2] << 16);
-    const u32x4 q = {v, v, v, v};
-    // 128 B per entry; rotate the 16-B pieces by lane so that each 8-lane
-    // store group covers all 32 banks
-#pragma unroll
-    for (int i = 0; i < PIECES; ++i) {
-      const int piece = (i + (int)threadIdx.x) & (PIECES - 1);
-      reinterpret_cast<u32x4 *>(s_tab)[e * PIECES + piece] = q;
-    }
-  }
-}
-
 // Fills the LDS byte table from a precomputed device table entry `v` (entry
 // e = threadIdx.x, already repeated 4 times: one 16-B store covers 4 bank
-// copies).  The 8 stores of a thread are rotated by its lane so that each
+// copies).  The stores of a thread are rotated by its lane so that each
 // 8-lane store group covers all 32 banks.  (Loading 8 pieces per thread to
 // make every store address an immediate offset was measured slower: the
 // extra loads delay the first weight loads.)
@@ -757,7 +419,7 @@ __device__ __forceinline__ int lut_shift(const float *lut) {
 }
 
 // Builds the CL (exact-code) byte table from a runtime fp32 codebook: entry
-// e = {hi pair, lo pair} of (code[e >> 4], code[e & 15]) * 2^S, 16 copies.
+// e = {hi pair, lo pair} of (code[e >> 4], code[e & 15]) * 2^S.
 template <int NT, int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const float *lut, int S) {
   for (int e = threadIdx.x; e < 256; e += NT) {
@@ -771,7 +433,7 @@ __device__ __forceinline__ void build_byte_table_exact(uint32_t *s_tab, const fl
 }
 
 // Builds the bf16 byte table from a runtime fp32 codebook: entry e = {hi pair, lo pair} of
-// (code[e >> 4], code[e & 15]) as bf16 hi + lo (c = hi + lo to ~2^-16), 16 copies.
+// (code[e >> 4], code[e & 15]) as bf16 hi + lo (c = hi + lo to ~2^-16).
 template <int NT, int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void build_byte_table_bf16(uint32_t *s_tab, const float *lut) {
   for (int e = threadIdx.x; e < 256; e += NT) {
@@ -784,7 +446,7 @@ __device__ __forceinline__ void build_byte_table_bf16(uint32_t *s_tab, const flo
   }
 }
 
-// The fp32 byte table from a runtime codebook: entry e = {code[e >> 4], code[e & 15]}, 16 copies.
+// The fp32 byte table from a runtime codebook: entry e = {code[e >> 4], code[e & 15]}.
 template <int NT, int PIECES = kTabCopies / 4>
 __device__ __forceinline__ void build_byte_table_f32(uint32_t *s_tab, const float *lut) {
   for (int e = threadIdx.x; e < 256; e += NT) {
@@ -796,14 +458,27 @@ __device__ __forceinline__ void build_byte_table_f32(uint32_t *s_tab, const floa
 // One step's worth of loads for R rows.  Branch-free: out-of-range rows and
 // the inactive tail lanes of the last step read a clamped in-bounds address
 // and are zeroed at compute time, so the compiler issues every load up front
-// (no exec-masked regions, no lazily re-read kernel arguments).
-template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = false> struct StepLoads {
+// (no exec-masked regions, no lazily re-read kernel arguments).  The lane's x
+// slice (32 activations) is loaded raw, so the loads retire in issue order; NOX:
+// x comes from an LDS image instead (the fused pre-norm).
+template <bool DQ, int DT, int R, bool NOX, bool FS> struct StepLoads {
+  static constexpr int kXWords = DT == QZ_DT_F32 ? 32 : 16;  // raw x dwords per lane
   u32x4 wv[R];
   uint32_t q[R];    // DQ: 8-bit scale code
   float a[R];       // DQ: absmax2 entry; else: fp32 absmax
-  XSlice<MODE, DT> xs;
+  uint32_t xr[kXWords];
   int xb;  // first activation index of this lane's chunk
   bool on;
+
+  __device__ __forceinline__ void load_x(const void *x, uint32_t e0) {
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(x) +
+                                                     e0 * (DT == QZ_DT_F32 ? 4u : 2u));
+#pragma unroll
+    for (int i = 0; i < kXWords / 4; ++i) {
+      const u32x4 v = p[i];
+      xr[4 * i] = v.x; xr[4 * i + 1] = v.y; xr[4 * i + 2] = v.z; xr[4 * i + 3] = v.w;
+    }
+  }
 
   // All offsets are 32-bit unsigned (the launcher guarantees M*K < 2^32): the
   // loads then use the SGPR-base + 32-bit VGPR offset form, with no 64-bit
@@ -817,11 +492,7 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
     on = boff_raw < (uint32_t)row_bytes;
     const uint32_t boff = on ? boff_raw : 0u;
     xb = 2 * (int)boff;
-    if constexpr (!XL && !(ABL & 2)) xs.load(p.x, 2u * boff);
-    if constexpr (ABL & 2) {
-#pragma unroll
-      for (int i = 0; i < XSlice<MODE, DT>::kWords; ++i) xs.raw[i] = 0x3C003C00u ^ boff;
-    }
+    if constexpr (!NOX) load_x(p.x, 2u * boff);
     // per row: weights then that row's scale, so row r can be consumed while
     // rows > r are still in flight (vmcnt retires in issue order)
 #pragma unroll
@@ -830,10 +501,7 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
       const unsigned char *rowp = p.B + (size_t)row * (uint32_t)row_bytes;
       wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + boff));
       const uint32_t b = (uint32_t)p.block_base + ((row * (uint32_t)p.K + 2u * boff) >> p.bs_log2);
-      if constexpr (ABL & 1) {
-        q[r] = b & 255u;
-        a[r] = 1.0f;
-      } else if constexpr (DQ) {
+      if constexpr (DQ) {
         q[r] = p.sc.qabsmax[b];
         a[r] = p.sc.absmax2[b >> p.bs2_log2];
       } else {
@@ -851,9 +519,7 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
     const uint32_t boff = ((uint32_t)s << 10) + ((uint32_t)lane << 4);
     on = true;
     xb = 2 * (int)boff;
-    // ABL & 2048 (microbenchmark only): every wave reads its own one of 64 copies of x
-    const void *xp = (ABL & 2048) ? (const void *)((const char *)p.x + (size_t)((row0 / R) & 63) * p.K * 2) : p.x;
-    if constexpr (!XL && !(ABL & 2)) xs.load(xp, 2u * boff);
+    if constexpr (!NOX) load_x(p.x, 2u * boff);
     const uint32_t lb = (2u * boff) >> p.bs_log2;                 // lane's block within the row
     const uint32_t sb = ((uint32_t)s << 11) >> p.bs_log2;         // step's first block within the row
     const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;              // blocks per row
@@ -863,10 +529,7 @@ template <int MODE, bool DQ, int DT, int R, bool XL, int ABL = 0, bool FS = fals
       const unsigned char *rowp = p.B + (size_t)row * (uint32_t)row_bytes;
       wv[r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + boff));
       const uint32_t rb = (uint32_t)p.block_base + row * bpr;    // wave-uniform
-      if constexpr (ABL & 1) {
-        q[r] = lb & 255u;
-        a[r] = 1.0f;
-      } else if constexpr (DQ) {
+      if constexpr (DQ) {
         q[r] = (p.sc.qabsmax + rb)[lb];
         typedef const __attribute__((address_space(4))) float *cfp;
         a[r] = ((cfp)p.sc.absmax2)[(rb + sb) >> p.bs2_log2];
@@ -947,71 +610,40 @@ struct GemvGroup {
   int total;
 };
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, bool NRM = false, bool PAIR = false, int FMV = 0, int OPT = 0,
-          bool PF = false, bool PS = false, int NSW = 0, bool GPS = false>
-__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block,
-                                          const GemvParams *pair = nullptr, const GemvGroup *grp = nullptr) {
-  // NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image
-  static_assert(!NRM || (NW == 4 && FS && !XL && MODE == kModeTab && (DT == QZ_DT_F16 || DT == QZ_DT_BF16)),
-                "fused pre-norm: 4 waves, full steps, 16-bit activations");
-  // PAIR (LlamaMLP's gate/up): waves 0-1 take R-row groups of pair[0] (gate_proj), waves 2-3 the
-  // same rows of pair[1] (up_proj); the epilogue stores act_fn(gate) * up (k_silu_mul's
-  // arithmetic) for those rows into pair[0].y, the input of down_proj
-  static_assert(!PAIR || (NW == 4 && WK == 1 && MODE == kModeTab && DT != QZ_DT_F32), "pair: 4 waves, WK = 1");
-  // WT ("wide table"): 256 B per byte value -- 64 copies of a 4-B entry, or 32 copies of an
-  // 8-B exact entry, 64 KiB -- so the lookup address is one v_perm and every copy is bank-private
+// The decode GEMV body.
+//  DQ: double-quantised scales; DT: activation dtype; R rows per wave; WK waves along K; NW waves
+//  per workgroup; FS: full-step loads (host-checked); CL: exact codes (fp16 x); WT: the 256-B-entry
+//  table; NRM: x is RMSNorm'd in the prologue (bit-identical to qz_rmsnorm) into an LDS image;
+//  PAIR (LlamaMLP's gate/up): waves 0-1 take R-row groups of pair[0] (gate_proj), waves 2-3 the
+//  same rows of pair[1] (up_proj), and the epilogue stores act_fn(gate) * up (k_silu_mul's
+//  arithmetic) into pair[0].y, the input of down_proj; TWO: the wave owns exactly two K-steps
+//  (host-checked) and runs them as straight-line code -- issue, barrier, issue step 2, decode,
+//  decode -- with no loop whose shared dominator would take the waits of step 1's scale codes above
+//  step 2's issue (profiles/r4_gemv_two_step.txt); PS (pair launches with the norm): persistent
+//  workgroups -- each takes row blocks blockIdx.x, + gridDim.x, ..., so its prologue (byte table,
+//  code2, the normalised x) is paid once, and the next block's first step is issued before the
+//  current block's epilogue.
+template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, bool NRM, bool PAIR, bool TWO, bool PS,
+          int STAMP = 0>
+__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block, const GemvParams *pair = nullptr) {
+  static_assert(!NRM || (NW == 4 && FS && DT != QZ_DT_F32), "fused pre-norm: 4 waves, full steps, 16-bit activations");
+  static_assert(!PAIR || (NW == 4 && WK == 1 && DT != QZ_DT_F32), "pair: 4 waves, WK = 1, 16-bit activations");
+  static_assert(!PS || (PAIR && TWO), "persistent form: two-step pair launches");
+  static_assert(!TWO || (FS && WK == 1), "two-step form: full steps, whole rows per wave");
+  static_assert(!CL || DT == QZ_DT_F16, "exact codes are the fp16-activation table");
+  static_assert(NW * 64 >= 256, "one byte-table entry per thread");
   constexpr int kPieces = WT ? 16 : kTabCopies / 4;
-  static_assert(!CL || MODE == kModeTab, "exact codes need the byte-table decode");
   QZ_STAMP_DECL;
   QZ_STAMP(0);
   const GemvParams p = load_params(p_in);
   constexpr int RG = NW / WK;
-  constexpr bool kSplit = XSlice<MODE, DT>::kSplit;   // fp32 x: hi + lo parts
-  // bf16 x (byte-table decode): bf16 code pairs hi + lo in 64-bit entries, the CL geometry
-  constexpr bool kBF = XSlice<MODE, DT>::kRawBF;
-  constexpr bool kF32 = XSlice<MODE, DT>::kRawF32;    // fp32 x: fp32 code table, v_fma_f32
-  constexpr bool kWide = CL || kBF || kF32;
-  // FMV (exact codes, fp16 x): 0 = hi + lo fp16 code pairs by v_dot2c; 1 = fp32 codes by
-  // v_fma_mix_f32 (chunk_dot_tab_fm), two-VALU addresses; 2 = the same on the 256-B-entry (WT)
-  // table with one-SDWA addresses
-  constexpr bool kFM = CL && DT == QZ_DT_F16 && (FMV == 1 || FMV == 2);
-  // FMV 3 / 4: fp32 codes against x widened to fp32 once per step, v_fma_f32 / v_pk_fma_f32
-  // (chunk_dot_tab_xf); the 128-B-entry kRawF32 table, two-VALU addresses
-  constexpr bool kXF = CL && DT == QZ_DT_F16 && (FMV == 3 || FMV == 4);
-  static_assert(FMV != 2 || WT, "SDWA addresses index the 256-B-entry table");
-  // OPT (round 4): bit 0 = issue the wave's second K-step before the prologue barrier (both steps
-  // of a K = 4096 row in flight from the start); bit 1 = build the fp16 byte-table entry from the
-  // SGPR byte planes (tab / tab_lo) instead of loading it (no global load gates the barrier)
-  constexpr bool kEarly = (OPT & 1) != 0;
-  constexpr bool kSTab = (OPT & 2) != 0 && MODE == kModeTab && !kBF && !kF32 && !kFM;
-  // bit 2: the scale codes / absmax2 of a step become visible only inside consume() (an empty asm),
-  // so hipcc cannot hoist their use -- and the vmcnt wait it needs -- above the next step's issue
-  constexpr bool kLaunder = (OPT & 4) != 0;
-  // bit 3: the wave owns exactly two K-steps (host-checked): straight-line code -- issue, barrier,
-  // issue step 2, decode, decode -- with no loop whose shared dominator would take the waits of
-  // step 1's scale codes above step 2's issue (hipcc did: the product's K = 4096 waves waited for
-  // ALL of step 1 before issuing step 2)
-  constexpr bool kTwo = (OPT & 8) != 0;
-  // PS (round 4, pair launches): persistent workgroups -- the grid is smaller than the row blocks and
-  // each workgroup takes blocks blockIdx.x, + gridDim.x, ..., so its prologue (byte table, code2,
-  // the fused RMSNorm of x into LDS) is paid once for all of them; the next block's first step is
-  // issued before the current block's epilogue
-  static_assert(!PS || (PAIR && kTwo && !kEarly && !PF), "persistent form: two-step pair launches");
-  // GPS (round 4, grouped launches with the fused norm): the same persistence over the blocks of all
-  // segments; a workgroup that crosses into another segment re-stages that segment's code2 table
-  static_assert(!GPS || (!PAIR && !PS && kTwo && !kEarly && !PF && WK == 1 && NW == 4), "grouped persistent form");
-  // bits 4 / 5 (round 4): a ring of 3 / 4 step buffers for waves that own exactly NSW K-steps
-  // (host-checked; K = 14336: Llama-3-8B down_proj, 7 steps), straight-line: step i + D - 1 is
-  // issued before step i is decoded, so D - 1 steps stay in flight instead of one
-  constexpr int kRing = (OPT & 32) ? 4 : (OPT & 16) ? 3 : 0;
-  static_assert(kRing == 0 || (NSW >= 2 && !kEarly && !kTwo && !PS && !PF), "ring: a fixed step count");
-  constexpr bool kScaled = XSlice<MODE, DT>::kScaled; // fp32/bf16 x: per-chunk power-of-two pre-scale
-  constexpr int XB = DT == QZ_DT_F32 ? 4 : 2;
+  constexpr bool kBF = DT == QZ_DT_BF16;    // bf16 code pairs hi + lo in 64-bit entries
+  constexpr bool kF32 = DT == QZ_DT_F32;    // fp32 code table, v_fma_f32
+  constexpr bool kWide = CL || kBF || kF32; // 64-bit entries
   __shared__ float s_code2[PAIR ? 2 : 1][DQ ? 256 : 1];   // PAIR: each weight's own double-quant code
   __shared__ float s_part[NW][R];
   __shared__ float s_part2[PS ? 2 : 1][NW][R];   // PS: by block parity (no barrier after the reads)
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[MODE == kModeTab ? (WT ? 2 : 1) * kTabDwords : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[(WT ? 2 : 1) * kTabDwords];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_x[];
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -1025,13 +657,9 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
 
-  // ABL & 32768 (microbenchmark, timing only: WRONG outputs): a prologue without memory -- the
-  // byte table from the SGPR planes, code2 / offset replaced by constants -- to price the
-  // prologue's global loads (which queue behind the CU's HBM requests)
-  constexpr bool kNoPro = (ABL & 32768) != 0;
   // 1. the double-quant code table load goes out first (it gates the barrier)
   float c2 = 0.0f, c2b = 0.0f, offset = 0.0f;
-  if constexpr (DQ && !kNoPro) {
+  if constexpr (DQ) {
     if constexpr (PAIR) {
       c2 = keep_sp(pair[0].sc.code2)[threadIdx.x];
       c2b = keep_sp(pair[1].sc.code2)[threadIdx.x];
@@ -1039,58 +667,17 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       c2 = p.sc.code2[threadIdx.x & 255];
     }
     offset = *p.sc.offset;
-  } else if constexpr (DQ) {
-    c2 = (float)(threadIdx.x & 255) * (1.0f / 256.0f);
   }
   // 1b. the precomputed byte-table entry of this thread (issued before the
   // weights, so waiting for it does not wait for the first HBM step)
   u32x4 tab_entry = {0u, 0u, 0u, 0u};
-  if constexpr (kSTab) {
-    if (!p.lut && threadIdx.x < 256) {
-      uint32_t P[4], tp[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) tp[i] = p.tab[i];
-      decode_lut16((uint32_t)threadIdx.x, tp, P);
-      const uint32_t h = (P[0] & 0xFFFFu) | (P[2] << 16);
-      if constexpr (CL) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) tp[i] = p.tab_lo[i];
-        decode_lut16((uint32_t)threadIdx.x, tp, P);
-        const uint32_t l = (P[0] & 0xFFFFu) | (P[2] << 16);
-        tab_entry = u32x4{h, l, h, l};
-      } else {
-        tab_entry = u32x4{h, h, h, h};
-      }
-    }
-  } else if constexpr (kNoPro && MODE == kModeTab) {
-    uint32_t P[4], tp[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) tp[i] = p.tab[i];
-    decode_lut16((uint32_t)threadIdx.x, tp, P);
-    const uint32_t h = (P[0] & 0xFFFFu) | (P[2] << 16);
-    tab_entry = u32x4{h, h, h, h};
-  } else if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    static_assert(NW * 64 >= 256, "one byte-table entry per thread");
-    if (!p.lut && threadIdx.x < 256) {
-      const ByteTable *bt = (kF32 || kFM || kXF) ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
-                            : kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
-                                  : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
-      tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
-    }
+  if (!p.lut && threadIdx.x < 256) {
+    const ByteTable *bt = kF32 ? (p.tabsel ? &g_byte_tab_fp4_f32 : &g_byte_tab_nf4_f32)
+                          : kBF ? (p.tabsel ? &g_byte_tab_fp4_bf : &g_byte_tab_nf4_bf)
+                                : (CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4));
+    tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
   }
-  // 1c. XL: this thread's share of x (<= kXLChunks 16-B chunks), also ahead of the weights
-  constexpr int kXLChunks = XL ? 8 : 1;
-  u32x4 xr[kXLChunks];
-  const int x_nchunk = (p.K * XB) >> 4;
-  if constexpr (XL) {
-#pragma unroll
-    for (int i = 0; i < kXLChunks; ++i) {
-      const int c = (int)threadIdx.x + i * NW * 64;
-      if (c < x_nchunk) xr[i] = reinterpret_cast<const u32x4 *>(p.x)[c];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // 1d. NRM: this thread's chunks of x and of the norm weight (L2-resident), ahead of the
+  // 1c. NRM: this thread's chunks of x and of the norm weight (L2-resident), ahead of the
   // weights.  The first kNHeld chunks (K <= 4096: all of them) stay in registers across the
   // barrier; later ones are read again after it (registers would cost occupancy)
   constexpr int kNChunks = NRM ? 8 : 1;   // up to 8 x 256 chunks of 8: K <= 16384
@@ -1111,16 +698,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     __builtin_amdgcn_sched_barrier(0);
   }
   // 2. this wave's first step of HBM traffic
-  StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> cur, other;
+  typedef StepLoads<DQ, DT, R, NRM, FS> Loads;
+  Loads cur, other;
   int s = wk;
   cur.issue(p, row0, s < nsteps ? s : 0, lane, row_bytes);
   const bool have = s < nsteps;
   const int n_my = have ? (nsteps - wk + WK - 1) / WK : 0;  // this wave's steps: s = wk, wk + WK, ...
-  if constexpr (kEarly) {
-    // unconditional (a clamped step when there is no second one): a conditional issue makes hipcc's
-    // waitcnt before the table stores count only the loads common to both paths, i.e. wait for step 0
-    other.issue(p, row0, n_my >= 2 ? s + WK : (s < nsteps ? s : 0), lane, row_bytes);
-  }
   // 3. stage the code table (waits only for the code load: it was issued first)
   if constexpr (DQ) {
     if (NW * 64 == 256 || threadIdx.x < 256) s_code2[0][threadIdx.x & 255] = c2;
@@ -1135,59 +718,35 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     ss = norm_wave_sum(ss);
     if (lane == 0) s_nss[wave] = ss;
   }
-  if constexpr (XL) {  // x -> LDS (the launcher guarantees K * XB <= kXLChunks * 16 * NW * 64)
-#pragma unroll
-    for (int i = 0; i < kXLChunks; ++i) {
-      const int c = (int)threadIdx.x + i * NW * 64;
-      if (c < x_nchunk) reinterpret_cast<u32x4 *>(s_x)[c] = xr[i];
-    }
-  }
-  uint32_t t[8];
-  if (MODE != kModeTab && p.lut) {  // register decodes (microbenchmarks): runtime codebook -> fp16 byte planes
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t h = __half_as_ushort(__float2half_rn(p.lut[i]));
-      t[i >> 2] |= (h & 0xFFu) << (8 * (i & 3));
-      t[4 + (i >> 2)] |= (h >> 8) << (8 * (i & 3));
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = p.tab[i];
-  }
   // output scale: the codebook's (FP4 x12: 1/12; exact NF4: 2^-14), or for a
-  // runtime codebook (always exact codes) 2^-S of its in-kernel split
+  // runtime codebook (fp16 x: always exact codes) 2^-S of its in-kernel split
   float out_scale = p.out_scale;
-  if constexpr (MODE == kModeTab && (ABL & 64) == 0) {
-    if constexpr (kF32 || kFM || kXF) {
-      if (p.lut) {
-        out_scale = 1.0f;
-        build_byte_table_f32<NW * 64, kPieces>(s_tab, p.lut);
-      } else if (threadIdx.x < 256) {
-        store_byte_table_entry<kPieces>(s_tab, tab_entry);
-      }
-    } else if constexpr (kBF) {
-      if (p.lut) {
-        out_scale = 1.0f;
-        build_byte_table_bf16<NW * 64, kPieces>(s_tab, p.lut);
-      } else if (threadIdx.x < 256) {
-        store_byte_table_entry<kPieces>(s_tab, tab_entry);
-      }
-    } else if constexpr (CL) {
-      if (p.lut) {
-        const int S = lut_shift(p.lut);
-        out_scale = ldexpf(1.0f, -S);
-        build_byte_table_exact<NW * 64, kPieces>(s_tab, p.lut, S);
-      } else if (threadIdx.x < 256) {
-        store_byte_table_entry<kPieces>(s_tab, tab_entry);
-      }
-    } else {
-      if (p.lut) build_byte_table<NW * 64, kPieces>(s_tab, t);
-      else if (threadIdx.x < 256) store_byte_table_entry<kPieces>(s_tab, tab_entry);
+  if constexpr (kF32) {
+    if (p.lut) {
+      out_scale = 1.0f;
+      build_byte_table_f32<NW * 64, kPieces>(s_tab, p.lut);
+    } else if (threadIdx.x < 256) {
+      store_byte_table_entry<kPieces>(s_tab, tab_entry);
     }
+  } else if constexpr (kBF) {
+    if (p.lut) {
+      out_scale = 1.0f;
+      build_byte_table_bf16<NW * 64, kPieces>(s_tab, p.lut);
+    } else if (threadIdx.x < 256) {
+      store_byte_table_entry<kPieces>(s_tab, tab_entry);
+    }
+  } else if constexpr (CL) {
+    if (p.lut) {
+      const int S = lut_shift(p.lut);
+      out_scale = ldexpf(1.0f, -S);
+      build_byte_table_exact<NW * 64, kPieces>(s_tab, p.lut, S);
+    } else if (threadIdx.x < 256) {
+      store_byte_table_entry<kPieces>(s_tab, tab_entry);
+    }
+  } else if (threadIdx.x < 256) {   // fp16 codes: the built-in books only (a runtime book is exact)
+    store_byte_table_entry<kPieces>(s_tab, tab_entry);
   }
-  if constexpr ((DQ || XL || MODE == kModeTab) && (ABL & 128) == 0) __syncthreads();
+  __syncthreads();
   if constexpr (NRM) {  // rs as k_rmsnorm (torch MeanOps: sum * (1/N), then rsqrt(var + eps)); x' -> LDS
     const float tot = __fadd_rn(__fadd_rn(s_nss[0], s_nss[1]), __fadd_rn(s_nss[2], s_nss[3]));
     const float rs = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)p.K), p.eps));
@@ -1209,43 +768,15 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  uint32_t ad[16];   // FMV = 2: per-byte address registers, byte 0 = jb for the whole kernel
-#pragma unroll
-  for (int i = 0; i < 16; ++i) ad[i] = jb;
 
-  // Steady state: the next step's loads are issued UNCONDITIONALLY before the
-  // current step is consumed, and the last step is peeled after the loop.  (A
-  // conditional prefetch makes hipcc's waitcnt pass pick the count valid on
-  // both paths -- vmcnt(0) -- which waits for the prefetch itself and
-  // serialises HBM traffic with the decode.)
-  typedef StepLoads<MODE, DQ, DT, R, XL || NRM, ABL, FS> Loads;
   auto consume = [&](const Loads &c) {
-    if constexpr (kLaunder) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        asm volatile("" : "+v"(const_cast<Loads &>(c).q[r]));
-        asm volatile("" : "+v"(const_cast<Loads &>(c).a[r]));
-      }
-    }
-    if constexpr (XL) const_cast<Loads &>(c).xs.load_lds(s_x, c.xb);
     if constexpr (NRM) {
-      auto &raw = const_cast<Loads &>(c).xs.raw;
+      auto &xr = const_cast<Loads &>(c).xr;
       const uint32_t c0 = (uint32_t)c.xb >> 3;  // the lane's first chunk
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const u32x4 v = *reinterpret_cast<const u32x4 *>(s_x + norm_x_off(c0 + (uint32_t)i));
-        raw[4 * i] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
-      }
-    }
-    uint32_t hi[16], lo[kSplit ? 16 : 1];
-    float usc;
-    c.xs.prepare(hi, lo, usc);
-    f32x2_t xf[kXF ? 16 : 1];
-    if constexpr (kXF) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const auto h = __builtin_bit_cast(h2_t, hi[i]);
-        xf[i] = f32x2_t{(float)h.x, (float)h.y};
+        xr[4 * i] = v.x; xr[4 * i + 1] = v.y; xr[4 * i + 2] = v.z; xr[4 * i + 3] = v.w;
       }
     }
 #pragma unroll
@@ -1254,13 +785,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[cb][c.q[r]], c.a[r]), offset);
       else am = c.a[r];
       am = c.on ? am : 0.0f;
-      if constexpr (kScaled) am *= usc;  // exact: a power of two (the lane's x pre-scale)
       float d;
-      if constexpr (kF32) d = chunk_dot_tab_f32(c.wv[r], c.xs.raw, s_tab, jb);
-      else if constexpr (kFM) d = chunk_dot_tab_fm<FMV == 2 ? 1 : 0>(c.wv[r], hi, s_tab, jb, ad);
-      else if constexpr (kXF) d = chunk_dot_tab_xf<FMV == 4 ? 1 : 0>(c.wv[r], xf, s_tab, jb);
-      else if constexpr (MODE == kModeTab) d = chunk_dot_tab<kSplit, ABL, kWide, WT, kBF>(c.wv[r], hi, lo, s_tab, jb);
-      else d = chunk_dot<MODE, kSplit>(c.wv[r], hi, lo, t);
+      if constexpr (kF32) {
+        d = chunk_dot_tab_f32(c.wv[r], c.xr, s_tab, jb);
+      } else {
+        d = chunk_dot_tab<kWide, WT, kBF>(c.wv[r], c.xr, s_tab, jb);
+      }
       acc[r] = fmaf(d, am, acc[r]);
     }
   };
@@ -1269,110 +799,11 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   // the two tails into one block fed by register COPIES, and copying a
   // register whose load is in flight forces vmcnt(0) -- the prefetch is then
   // waited for before the current step is decoded.  Every consume(cur) below
-  // reads the same registers on every path, so no copies are needed.
-  // PF: this wave's share of the next launch's first K-steps, issued after its own last loads (so no
-  // wait for its own data waits for them); the values are discarded after the stores
-  constexpr int kPfMax = PF ? 4 : 1;
-  uint32_t pfv[kPfMax];
-  auto prefetch = [&]() {
-    if constexpr (PF) {
-      const int W = (int)gridDim.x * NW, gw = block * NW + wave;
-      const int items = p.pf_rows * p.pf_chunks;
-#pragma unroll
-      for (int i = 0; i < kPfMax; ++i) {
-        const int it = min(gw + i * W, items - 1);
-        const int r = it / p.pf_chunks, ck = it - r * p.pf_chunks;
-        const uint32_t off = (uint32_t)r * p.pf_row_bytes + ((uint32_t)ck << 10) + ((uint32_t)lane << 4);
-        pfv[i] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p.pf + off));
-      }
-    }
-  };
-  if constexpr (GPS) {
-    auto seg_of = [&](int b) {
-      int sg = 0;
-#pragma unroll
-      for (int i = 1; i < kMaxSeg; ++i)
-        if (i < grp->nseg && b >= grp->start[i]) sg = i;
-      return __builtin_amdgcn_readfirstlane(sg);
-    };
-    auto store_rows = [&](const GemvParams &q, int r0) {
-      float v[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
-      if (lane == kWave - 1) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int row = r0 + r;
-          if (row < q.M) {
-            float o = v[r] * out_scale;
-            if (q.bias) o += load_f32<DT>(q.bias, row);
-            o = add_res<DT>(o, q.res, row);
-            store_f32<DT>(q.y, row, o);
-          }
-        }
-      }
-    };
-    const int total = grp->total;
-    int blk = (int)blockIdx.x;
-    int sg = seg_of(blk);
-    GemvParams q = p;
-    for (int it = 0;; ++it) {
-      other.issue(q, row0, s + WK, lane, row_bytes);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(cur);
-      consume(other);
-      const int nb = blk + (int)gridDim.x;   // workgroup-uniform
-      if (nb >= total) {
-        store_rows(q, row0);
-        break;
-      }
-      const int ns = seg_of(nb);
-      const GemvParams qn = load_params(grp->seg[ns]);
-      const int nrow0 = ((nb - grp->start[ns]) * RG + rg) * R;
-      cur.issue(qn, nrow0, s, lane, row_bytes);   // the next block's first step, ahead of this epilogue
-      __builtin_amdgcn_sched_barrier(0);
-      store_rows(q, row0);
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-      if (ns != sg) {   // another segment: its own code2 table and offset
-        if constexpr (DQ) {
-          __syncthreads();   // every wave has decoded the old segment's blocks
-          s_code2[0][threadIdx.x & 255] = qn.sc.code2[threadIdx.x & 255];
-          offset = *qn.sc.offset;
-          __syncthreads();
-        }
-        sg = ns;
-      }
-      q = qn;
-      blk = nb;
-      row0 = nrow0;
-    }
-    return;
-  } else if constexpr (kRing > 0) {
-    Loads third, fourth;
-    auto sel = [&](auto K) -> Loads & {
-      constexpr int k = decltype(K)::value;
-      if constexpr (k == 0) return cur;
-      else if constexpr (k == 1) return other;
-      else if constexpr (k == 2) return third;
-      else return fourth;
-    };
-    gv_static_for<NSW>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      if constexpr (i == 0) {
-        gv_static_for<kRing - 1>([&](auto J) {
-          constexpr int j = decltype(J)::value + 1;
-          if constexpr (j < NSW) sel(std::integral_constant<int, j % kRing>{}).issue(p, row0, s + j * WK, lane, row_bytes);
-        });
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (i + kRing - 1 < NSW) {
-        constexpr int j = i + kRing - 1;
-        sel(std::integral_constant<int, j % kRing>{}).issue(p, row0, s + j * WK, lane, row_bytes);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      consume(sel(std::integral_constant<int, i % kRing>{}));
-    });
-  } else if constexpr (PS) {
+  // reads the same registers on every path, so no copies are needed.  The next
+  // step's loads are issued UNCONDITIONALLY before the current step is consumed
+  // (a conditional prefetch makes hipcc's waitcnt pass pick the count valid on
+  // both paths -- vmcnt(0) -- which serialises HBM traffic with the decode).
+  if constexpr (PS) {
     // the pair epilogue of block `blk` (the one after the loop below, with s_part by parity)
     auto pair_out = [&](int blk, int par) {
       float v[R];
@@ -1419,39 +850,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       row0 = nrow0;
     }
     return;
-  } else if constexpr (kTwo && !kEarly) {
+  } else if constexpr (TWO) {
     other.issue(p, row0, s + WK, lane, row_bytes);
-    prefetch();
     __builtin_amdgcn_sched_barrier(0);
     consume(cur);
     QZ_STAMP(2);
     consume(other);
-  } else if (kEarly && have) {
-    // `other` already holds step s + WK (n >= 2); at the loop top cur = step j, other = j + 1
-    const int n = n_my;
-    int j = 0;
-    for (; j + 3 < n; j += 2) {
-      consume(cur);
-      cur.issue(p, row0, s + 2 * WK, lane, row_bytes);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(other);
-      other.issue(p, row0, s + 3 * WK, lane, row_bytes);
-      __builtin_amdgcn_sched_barrier(0);
-      s += 2 * WK;
-    }
-    if (n - j == 3) {
-      consume(cur);
-      cur.issue(p, row0, s + 2 * WK, lane, row_bytes);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(other);
-      consume(cur);
-    } else if (n - j == 2) {
-      consume(cur);
-      QZ_STAMP(2);
-      consume(other);
-    } else {
-      consume(cur);
-    }
   } else if (have) {
     const int n = n_my;
     int j = 0;
@@ -1466,22 +870,15 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     if (n - j == 2) {
       other.issue(p, row0, s + WK, lane, row_bytes);
-      prefetch();
       __builtin_amdgcn_sched_barrier(0);
       consume(cur);
       QZ_STAMP(2);
       consume(other);
     } else {
-      prefetch();
       consume(cur);
     }
   }
 
-  if constexpr ((ABL & 4) != 0) {  // benchmark-only: no reduction, no store
-#pragma unroll
-    for (int r = 0; r < R; ++r) asm volatile("" ::"v"(acc[r]));
-    return;
-  }
   QZ_STAMP(3);
   if constexpr (PAIR) {  // gate (waves 0-1) and up (waves 2-3) of the same rows meet in LDS
     float v[R];
@@ -1512,10 +909,10 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   if constexpr (WK == 1) {  // the wave owns whole rows: lane 63 reduces and stores them
     float v[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = (ABL & 8) ? acc[r] : wave_sum_last(acc[r]);
+    for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
     if (lane == kWave - 1) {
       // 16-bit outputs of a row pair inside M go out as one dword (row0 is even for even R)
-      constexpr bool kPack = DT != QZ_DT_F32 && R % 2 == 0 && (ABL & (1024 | 4096)) == 0;  // 4096: A/B knob
+      constexpr bool kPack = DT != QZ_DT_F32 && R % 2 == 0;
       const bool pack = kPack && row0 + R <= p.M && (reinterpret_cast<uintptr_t>(p.y) & 3u) == 0;
       if (pack) {
 #pragma unroll
@@ -1537,25 +934,18 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
             float o = v[r] * out_scale;
             if (p.bias) o += load_f32<DT>(p.bias, row);
             o = add_res<DT>(o, p.res, row);
-            if constexpr ((ABL & 1024) != 0 && DT == QZ_DT_F16)  // microbenchmark: non-temporal y store
-              __builtin_nontemporal_store((uint16_t)f32_to_f16_bits(o), reinterpret_cast<uint16_t *>(p.y) + row);
-            else
-              store_f32<DT>(p.y, row, o);
+            store_f32<DT>(p.y, row, o);
           }
         }
       }
     }
     QZ_STAMP(4);
     QZ_STAMP_FLUSH(block * NW + wave);
-    if constexpr (PF) {
-#pragma unroll
-      for (int i = 0; i < kPfMax; ++i) asm volatile("" ::"v"(pfv[i]));
-    }
     return;
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const float v = (ABL & 8) ? acc[r] : wave_sum_last(acc[r]);
+    const float v = wave_sum_last(acc[r]);
     if (lane == kWave - 1) s_part[wave][r] = v;
   }
   __syncthreads();
@@ -1573,393 +963,12 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   }
 }
 
-template <int MODE, bool DQ, int DT, int R, int WK, int NW = 4, bool XL = false, int ABL = 0, bool FS = false,
-          bool CL = false, bool WT = false, int FMV = 0, int OPT = 0, bool PF = false, int NSW = 0>
+template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, bool TWO, int STAMP = 0>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
-  gemv_body<MODE, DQ, DT, R, WK, NW, XL, ABL, FS, CL, WT, false, false, FMV, OPT, PF, false, NSW>(p, blockIdx.x);
+  gemv_body<DQ, DT, R, WK, NW, FS, CL, WT, false, false, TWO, false, STAMP>(p, blockIdx.x);
 }
 
-// Streaming ("persistent") form for rows of exactly NS K-steps (K = 2048 * NS, full-step
-// loads, fp16 x): a grid of at most the resident workgroups, each wave walks the row groups
-// u = gw, gw + W, gw + 2W, ... (gw = its global wave id, W = waves in the grid), R rows per
-// group.  The LDS byte table is filled once per workgroup, the wave's x slices of every step
-// stay in registers for all its row groups (x is loaded once per wave, not once per row group),
-// and the loads of group u + W are issued before group u is decoded, so the HBM stream of a
-// wave never stops between its row groups: only its last group has a serial decode tail.
-// Set A always holds step 0 of a group, set B step 1 (NS = 2).
-template <bool DQ, int R, bool CL, int ABL = 0>
-__device__ __forceinline__ void gemv_stream2_body(const GemvParams &p_in, int nunits) {
-  constexpr int NS = 2;
-  static_assert(NS == 2, "two named load sets, one per K-step");
-  typedef StepLoads<kModeTab, DQ, QZ_DT_F16, R, true, ABL, true> Loads;   // XL = true: no x loads
-  const GemvParams p = load_params(p_in);
-  __shared__ float s_code2[DQ ? 256 : 1];
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabDwords];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const int W = (int)gridDim.x * 4;
-  const int gw = (int)blockIdx.x * 4 + wave;
-  const int row_bytes = p.K >> 1;
-  // 1. the code table and this thread's byte-table entry go out first
-  float c2 = 0.0f, offset = 0.0f;
-  if constexpr (DQ) {
-    c2 = p.sc.code2[threadIdx.x & 255];
-    offset = *p.sc.offset;
-  }
-  const ByteTable *bt = CL ? &g_byte_tab_nf4x : (p.tabsel ? &g_byte_tab_fp4 : &g_byte_tab_nf4);
-  const u32x4 tab_entry = reinterpret_cast<const u32x4 *>(bt->v)[threadIdx.x];
-  // 2. the wave's first row group (both steps), then x (64 B per lane per step)
-  Loads A, B;
-  const int u0 = gw < nunits ? gw : nunits - 1;
-  A.issue(p, u0 * R, 0, lane, row_bytes);
-  B.issue(p, u0 * R, 1, lane, row_bytes);
-  XSlice<kModeTab, QZ_DT_F16> x0, x1;
-  x0.load(p.x, 2u * ((uint32_t)lane << 4));
-  x1.load(p.x, 2u * ((1u << 10) + ((uint32_t)lane << 4)));
-  if constexpr (DQ) s_code2[threadIdx.x & 255] = c2;
-  store_byte_table_entry(s_tab, tab_entry);
-  __syncthreads();
-  const uint32_t jb = CL ? (uint32_t)(lane & (kTabCopiesCL - 1)) << 3 : (uint32_t)(lane & 31) << 2;
-  float acc[R];
-  auto consume = [&](const Loads &c, const XSlice<kModeTab, QZ_DT_F16> &xs) {
-    uint32_t lo[1];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float am;
-      if constexpr (DQ) am = __fadd_rn(__fmul_rn(s_code2[c.q[r]], c.a[r]), offset);
-      else am = c.a[r];
-      const float d = chunk_dot_tab<false, ABL, CL>(c.wv[r], xs.raw, lo, s_tab, jb);
-      acc[r] = fmaf(d, am, acc[r]);
-    }
-  };
-  auto finish = [&](int row0) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = wave_sum_last(acc[r]);
-    if (lane == kWave - 1) {
-      if constexpr (R % 2 == 0) {
-        if (row0 + R <= p.M && (reinterpret_cast<uintptr_t>(p.y) & 3u) == 0) {
-#pragma unroll
-          for (int r = 0; r < R; r += 2) {
-            float o0 = acc[r] * p.out_scale, o1 = acc[r + 1] * p.out_scale;
-            if (p.bias) {
-              o0 += load_f32<QZ_DT_F16>(p.bias, row0 + r);
-              o1 += load_f32<QZ_DT_F16>(p.bias, row0 + r + 1);
-            }
-            reinterpret_cast<uint32_t *>(p.y)[(row0 + r) >> 1] = pack16<QZ_DT_F16>(o0, o1);
-          }
-          return;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (row0 + r < p.M) {
-          float o = acc[r] * p.out_scale;
-          if (p.bias) o += load_f32<QZ_DT_F16>(p.bias, row0 + r);
-          store_f32<QZ_DT_F16>(p.y, row0 + r, o);
-        }
-      }
-    }
-  };
-  if (gw >= nunits) return;
-  const int n = (nunits - gw + W - 1) / W;   // this wave's row groups
-  int u = gw;
-  for (int i = 0; i + 1 < n; ++i) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-    consume(A, x0);
-    A.issue(p, (u + W) * R, 0, lane, row_bytes);
-    __builtin_amdgcn_sched_barrier(0);
-    consume(B, x1);
-    finish(u * R);
-    B.issue(p, (u + W) * R, 1, lane, row_bytes);
-    __builtin_amdgcn_sched_barrier(0);
-    u += W;
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  consume(A, x0);
-  consume(B, x1);
-  finish(u * R);
-}
-
-template <bool DQ, int R, bool CL, int ABL = 0>
-__global__ __launch_bounds__(256) void k_gemv_4bit_stream2(GemvParams p, int nunits) {
-  gemv_stream2_body<DQ, R, CL, ABL>(p, nunits);
-}
-
-// ---------------------------------------------------------------------------
-// MFMA-product decode GEMV (round 4, experimental: k_gemv_4bit_mf).  The byte table's
-// entries ARE v_mfma_f32_16x16x32_f16 operand fragments: a lane's 16 packed bytes decode
-// through the table into 32 codes = four 8-code fragments with no VALU after the LDS read,
-// so the matrix pipe takes the products and the VALU keeps only the table addresses.
-//  * a wave owns a 16-row tile: lane l reads row (l & 15), 16-B chunk g = l >> 4 of each 64-B
-//    row segment; one load instruction covers 16 rows x 128 elements (1 KiB);
-//  * the codes are the B operand (lane l supplies B[k = 8 g + jj][n = l & 15]: weight row n,
-//    codes 8j..8j+7 of chunk g for MFMA j) and x is a "diagonal" A operand: A[m][8 g + jj] =
-//    x of chunk g if m == g, else 0 -- the lanes with (l & 15) == (l >> 4) load x, the others
-//    load zeros (a zero buffer, so no select and no exec mask);
-//  * so C[m = g][n = row] is chunk g's unscaled dot of that row, which the 16x16 C layout puts
-//    in lane `row` (0..15), register g: each of lanes 0..15 scales its row's four chunks by
-//    their blocks' absmax and keeps ONE running sum -- no cross-lane reduction;
-//  * exact codes add the lo fragments into the same C (hi + lo = the fp32 code to ~2^-23);
-//  * NWK waves split K; the per-row partials meet in LDS.
-// ---------------------------------------------------------------------------
-typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
-typedef float float4_t __attribute__((ext_vector_type(4)));
-__device__ const uint32_t g_mf_zeros[512] = {};   // the inactive lanes' A fragments (2 KiB of zeros)
-
-template <bool CL, bool WT, int NWK, int NL>
-__global__ __launch_bounds__(NWK * 64) void k_gemv_4bit_mf(GemvParams p_in) {
-  const GemvParams p = load_params(p_in);
-  constexpr int kPieces = WT ? 16 : kTabCopies / 4;
-  static_assert(NL % 2 == 0 && NL <= 8, "2 NL qabsmax bytes per row come as whole dwords");
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[(WT ? 2 : 1) * kTabDwords];
-  __shared__ float s_code2[256];
-  __shared__ float s_part[NWK][16];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int row0 = blockIdx.x * 16;
-  const int rl = lane & 15, g = lane >> 4;           // this lane's row in the tile, its 16-B chunk
-  const uint32_t row_bytes = (uint32_t)p.K >> 1;
-  // 1. code2 and the table entry (the barrier waits for them), then every weight load
-  float c2 = 0.0f;
-  if (threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x];
-  const float offset = *p.sc.offset;
-  u32x4 tab_entry = {0u, 0u, 0u, 0u};
-  if (threadIdx.x < 256) tab_entry = reinterpret_cast<const u32x4 *>((CL ? &g_byte_tab_nf4x : &g_byte_tab_nf4)->v)[threadIdx.x];
-  const uint32_t kb0 = (uint32_t)(wave * NL) * 64u;  // this wave's first byte within a row
-  const unsigned char *rowp = p.B + (size_t)(uint32_t)(row0 + rl) * row_bytes;
-  u32x4 wv[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i)
-    wv[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rowp + kb0 + 64u * i + 16u * g));
-  // x: A fragment (i, j) = 16 B at 4 kb0 + 64 g + 256 i + 16 j in the diagonal lanes, zeros elsewhere
-  typedef const __attribute__((address_space(1))) char *gcp;   // global, not flat, loads
-  u32x4 xa[NL][4];
-#pragma unroll
-  for (int i = 0; i < NL; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xa[i][j] = u32x4{0u, 0u, 0u, 0u};
-  if (rl == g) {   // four lanes load x (exec-masked: a quarter KiB per load, not a KiB of zeros)
-    const gcp xbase = (gcp)p.x + 4u * kb0 + 64u * (uint32_t)g;
-#pragma unroll
-    for (int i = 0; i < NL; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        xa[i][j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(xbase + 256 * i + 16 * j);
-  }
-  // scales of row (row0 + rl): its 2 NL blocks of this wave's range as NL / 2 dwords of qabsmax
-  const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;
-  const uint32_t b0 = (uint32_t)p.block_base + (uint32_t)(row0 + rl) * bpr + ((2u * kb0) >> p.bs_log2);
-  uint32_t qv[NL / 2];
-#pragma unroll
-  for (int t = 0; t < NL / 2; ++t) qv[t] = reinterpret_cast<const uint32_t *>(p.sc.qabsmax + b0)[t];
-  const float a2 = p.sc.absmax2[b0 >> p.bs2_log2];    // the 2 NL blocks share one (host-checked)
-  if (threadIdx.x < 256) {
-    s_code2[threadIdx.x] = c2;
-    store_byte_table_entry<kPieces>(s_tab, tab_entry);
-  }
-  __syncthreads();
-  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  const uint32_t jb = WT ? (uint32_t)(lane & 31) << 3 : (uint32_t)(lane & 15) << 3;
-  float acc = 0.0f;
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const uint32_t w[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
-    uint32_t hi[16], lo[16];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        uint32_t a;
-        if constexpr (WT) a = __builtin_amdgcn_perm(w[d], jb, 0x0C0C0000u | ((4u + m) << 8));
-        else a = ((m == 0 ? (w[d] << 7) : (w[d] >> (8 * m - 7))) & 0x7F80u) | jb;
-        if constexpr (CL) {
-          const u32x2 e = *reinterpret_cast<const u32x2 *>(tb + a);
-          hi[4 * d + m] = e.x;
-          lo[4 * d + m] = e.y;
-        } else {
-          hi[4 * d + m] = *reinterpret_cast<const uint32_t *>(tb + a);
-        }
-      }
-    }
-    float4_t c = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const half8_t af = __builtin_bit_cast(half8_t, xa[i][j]);
-      const u32x4 bh = {hi[4 * j], hi[4 * j + 1], hi[4 * j + 2], hi[4 * j + 3]};
-      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, __builtin_bit_cast(half8_t, bh), c, 0, 0, 0);
-      if constexpr (CL) {
-        const u32x4 bl = {lo[4 * j], lo[4 * j + 1], lo[4 * j + 2], lo[4 * j + 3]};
-        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, __builtin_bit_cast(half8_t, bl), c, 0, 0, 0);
-      }
-    }
-    // chunks 0, 1 of load i lie in block 2 i, chunks 2, 3 in block 2 i + 1 (bytes of qv)
-    const uint32_t qw = qv[i >> 1];
-    const float am0 = __fadd_rn(__fmul_rn(s_code2[(qw >> (16 * (i & 1))) & 0xFFu], a2), offset);
-    const float am1 = __fadd_rn(__fmul_rn(s_code2[(qw >> (16 * (i & 1) + 8)) & 0xFFu], a2), offset);
-    acc = fmaf(__fadd_rn(c[0], c[1]), am0, acc);
-    acc = fmaf(__fadd_rn(c[2], c[3]), am1, acc);
-  }
-  if (lane < 16) s_part[wave][lane] = acc;
-  __syncthreads();
-  if (threadIdx.x < 16) {
-    float v = 0.0f;
-#pragma unroll
-    for (int w = 0; w < NWK; ++w) v += s_part[w][threadIdx.x];
-    const int row = row0 + (int)threadIdx.x;
-    float o = v * p.out_scale;
-    if (p.bias) o += load_f32<QZ_DT_F16>(p.bias, row);
-    store_f32<QZ_DT_F16>(p.y, row, o);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// MFMA-diagonal decode GEMV (round 4, experimental: k_gemv_4bit_dg).  The product GEMV's memory
-// layout -- a wave reads ONE row per load instruction, contiguously -- with the products on
-// the matrix pipe:
-//  * a segment is 1024 elements (512 B) of a row; lane l owns its 16-element chunk
-//    c(l) = 4 (l & 15) + (l >> 4), i.e. 8 B at 8 c(l): one dwordx2 per lane per segment;
-//  * v_mfma_f32_16x16x32_f16 with the lane's codes as A (A[m = l & 15][k = 8 (l >> 4) + jj])
-//    and the lane's OWN x as B (B[k = 8 (l >> 4) + jj][n = l & 15]): C[m][n] sums the four k
-//    groups g of lanes m + 16 g (codes) against lanes n + 16 g (x), so the diagonal m == n is
-//    sum_g codes(chunk 4 m + g) . x(chunk 4 m + g) = the dot of scale block m of the segment
-//    (chunks 4m..4m+3 = elements 64m..64m+63): one absmax per diagonal element;
-//  * exact codes: an A fragment is two table entries as they land from two ds_read_b64,
-//    {hi pair, lo pair} of bytes 2f and 2f + 1 = codes (ch, ch, cl, cl, ch, ch, cl, cl), and B
-//    the matching x pairs doubled (x, x, x, x of 4f..4f+3 as (x0 x1 x0 x1 x2 x3 x2 x3)) -- built
-//    once per segment and shared by the R rows;
-//  * the diagonal C[m][m] sits in lane m + 16 (m >> 2), register m & 3: every lane scales its
-//    four C registers by its block's absmax into four running sums per row and keeps the one
-//    with index m & 3 at the end; 16 lanes x NWK waves meet in LDS.
-// ---------------------------------------------------------------------------
-template <bool CL, int R, int NSEG, int NWK>
-__global__ __launch_bounds__(NWK * 64) void k_gemv_4bit_dg(GemvParams p_in) {
-  const GemvParams p = load_params(p_in);
-  constexpr int kPieces = 16;   // the 256-B-entry (WT) table: 32 bank-private 8-B copies, one v_perm per address
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[2 * kTabDwords];
-  __shared__ float s_code2[256];
-  __shared__ float s_red[NWK][R][16];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int row0 = blockIdx.x * R;
-  const int m = lane & 15;                                   // this lane's C column = its diagonal row
-  const uint32_t c = 4u * (uint32_t)m + ((uint32_t)lane >> 4);  // this lane's 16-element chunk of a segment
-  const uint32_t row_bytes = (uint32_t)p.K >> 1;
-  // 1. code2 and the table entry first (the barrier waits for them)
-  float c2 = 0.0f;
-  if (threadIdx.x < 256) c2 = p.sc.code2[threadIdx.x];
-  const float offset = *p.sc.offset;
-  u32x4 tab_entry = {0u, 0u, 0u, 0u};
-  if (threadIdx.x < 256) tab_entry = reinterpret_cast<const u32x4 *>((CL ? &g_byte_tab_nf4x : &g_byte_tab_nf4)->v)[threadIdx.x];
-  // 2. weights (R rows x NSEG segments), x (the lane's chunk of each segment), scale codes
-  const uint32_t seg0 = (uint32_t)(wave * NSEG);               // this wave's first segment of the row
-  u32x2 wv[NSEG][R];
-#pragma unroll
-  for (int sg = 0; sg < NSEG; ++sg)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const unsigned char *rp = p.B + (size_t)(uint32_t)(row0 + r) * row_bytes + (seg0 + sg) * 512u + 8u * c;
-      wv[sg][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(rp));
-    }
-  u32x4 xr[NSEG][2];
-#pragma unroll
-  for (int sg = 0; sg < NSEG; ++sg) {
-    const u32x4 *xp = reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(p.x) + ((seg0 + sg) * 1024u + 16u * c) * 2u);
-    xr[sg][0] = xp[0];
-    xr[sg][1] = xp[1];
-  }
-  const uint32_t bpr = (uint32_t)p.K >> p.bs_log2;             // 64-element blocks per row
-  uint32_t qb[NSEG][R];
-  float a2[NSEG][R];
-#pragma unroll
-  for (int sg = 0; sg < NSEG; ++sg)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t b = (uint32_t)p.block_base + (uint32_t)(row0 + r) * bpr + (seg0 + sg) * 16u;   // the segment's first block
-      qb[sg][r] = p.sc.qabsmax[b + (uint32_t)m];
-      typedef const __attribute__((address_space(4))) float *cfp;
-      a2[sg][r] = ((cfp)p.sc.absmax2)[b >> p.bs2_log2];        // one per (row, segment): 16 | 256
-    }
-  if (threadIdx.x < 256) {
-    s_code2[threadIdx.x] = c2;
-    store_byte_table_entry<kPieces>(s_tab, tab_entry);
-  }
-  __syncthreads();
-  const unsigned char *tb = reinterpret_cast<const unsigned char *>(s_tab);
-  const uint32_t jb = (uint32_t)(lane & 31) << 3;
-  float4_t acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int sg = 0; sg < NSEG; ++sg) {
-    const uint32_t X[8] = {xr[sg][0].x, xr[sg][0].y, xr[sg][0].z, xr[sg][0].w,
-                           xr[sg][1].x, xr[sg][1].y, xr[sg][1].z, xr[sg][1].w};
-    half8_t bfr[CL ? 4 : 2];
-#pragma unroll
-    for (int f = 0; f < (CL ? 4 : 2); ++f) {
-      const u32x4 b = CL ? u32x4{X[2 * f], X[2 * f], X[2 * f + 1], X[2 * f + 1]}
-                         : u32x4{X[4 * f], X[4 * f + 1], X[4 * f + 2], X[4 * f + 3]};
-      bfr[f] = __builtin_bit_cast(half8_t, b);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t w[2] = {wv[sg][r].x, wv[sg][r].y};
-      float4_t cc = {0.0f, 0.0f, 0.0f, 0.0f};
-      if constexpr (CL) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const uint32_t wd = w[f >> 1];
-          const uint32_t b0 = (uint32_t)(2 * (f & 1)), b1 = b0 + 1u;
-          const u32x2 e0 = *reinterpret_cast<const u32x2 *>(tb + __builtin_amdgcn_perm(wd, jb, 0x0C0C0000u | ((4u + b0) << 8)));
-          const u32x2 e1 = *reinterpret_cast<const u32x2 *>(tb + __builtin_amdgcn_perm(wd, jb, 0x0C0C0000u | ((4u + b1) << 8)));
-          const u32x4 a = {e0.x, e0.y, e1.x, e1.y};
-          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), bfr[f], cc, 0, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          uint32_t h[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            h[t] = *reinterpret_cast<const uint32_t *>(tb + __builtin_amdgcn_perm(w[f], jb, 0x0C0C0000u | ((4u + t) << 8)));
-          const u32x4 a = {h[0], h[1], h[2], h[3]};
-          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8_t, a), bfr[f], cc, 0, 0, 0);
-        }
-      }
-      const float am = __fadd_rn(__fmul_rn(s_code2[qb[sg][r]], a2[sg][r]), offset);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc[r][k] = fmaf(cc[k], am, acc[r][k]);
-    }
-  }
-  // the diagonal: lane l keeps register m & 3 if m >> 2 == l >> 4 (its block's dot), else nothing
-  const bool diag = (m >> 2) == (lane >> 4);
-  const int k3 = m & 3;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const float v = k3 == 0 ? acc[r][0] : k3 == 1 ? acc[r][1] : k3 == 2 ? acc[r][2] : acc[r][3];
-    if (diag) s_red[wave][r][m] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < R * 16) {   // thread (r, b): the NWK partials of block column b of row r, then 16 lanes
-    const int r = threadIdx.x >> 4, b = threadIdx.x & 15;
-    float v = 0.0f;
-#pragma unroll
-    for (int wk = 0; wk < NWK; ++wk) v += s_red[wk][r][b];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
-    if (b == 0) {
-      const int row = row0 + r;
-      float o = v * p.out_scale;
-      if (p.bias) o += load_f32<QZ_DT_F16>(p.bias, row);
-      store_f32<QZ_DT_F16>(p.y, row, o);
-    }
-  }
-}
-
-
-template <int MODE, bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM = false, int OPT = 0, bool GPS = false,
-          bool WT = false>
+template <bool DQ, int DT, int R, int WK, bool FS, bool CL, bool NRM, bool TWO>
 __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   const int b = blockIdx.x;
   int s = 0;
@@ -1972,34 +981,15 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_grouped(GemvGroup g) {
   // laundering asm would serialise them (one s_waitcnt per field)
   const GemvParams seg = g.seg[s];
   const int start = g.start[s];
-  gemv_body<MODE, DQ, DT, R, WK, 4, false, 0, FS, CL, WT, NRM, false, 0, OPT, false, false, 0, GPS>(seg, b - start,
-                                                                                                 nullptr, &g);
-}
-
-// QZ_GROUPED_PS / QZ_GROUPED_WT (measurement knobs): persistent workgroups for the two-step grouped
-// launch with the fused norm (optionally on the 256-B-entry exact-code table)
-template <bool DQ, int DT, int R, bool CL, bool WT>
-static void launch_grouped_ps(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
-  if constexpr ((DT == QZ_DT_F16 || DT == QZ_DT_BF16) && (R == 1 || R == 2 || R == 4) && (!WT || (CL && DT == QZ_DT_F16)))
-    hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ, DT, R, 1, true, CL, true, 8, true, WT>), dim3(grid), dim3(256),
-                       lds, s, g);
+  gemv_body<DQ, DT, R, WK, 4, FS, CL, false, NRM, false, TWO, false>(seg, b - start);
 }
 
 // LlamaMLP's gate/up pair (gemv_body PAIR): one launch computes act_fn(gate_proj(x)) * up_proj(x)
-template <int MODE, bool DQ, int DT, int R, bool FS, bool CL, bool NRM, int OPT = 0, bool PS = false, bool WT = false>
+template <bool DQ, int DT, int R, bool CL, bool NRM, bool TWO, bool PS = false, bool WT = false>
 __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
-  gemv_body<MODE, DQ, DT, R, 1, 4, false, 0, FS, CL, WT, NRM, true, 0, OPT, false, PS>(seg, blockIdx.x, g.seg);
-}
-
-// QZ_PAIR_WT (measurement knob): the persistent exact-code pair on the 256-B-entry table (64 KiB: 32
-// bank-private copies of each 8-B entry, v_perm addresses), 2 workgroups per CU
-template <bool DQ, int DT, int R, bool CL, bool NRM>
-static void launch_pair_wt(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
-  if constexpr (CL && NRM && DT == QZ_DT_F16 && (R == 2 || R == 4))
-    hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ, DT, R, true, CL, NRM, 8, true, true>), dim3(grid), dim3(256), lds,
-                       s, g);
+  gemv_body<DQ, DT, R, 1, 4, true, CL, WT, NRM, true, TWO, PS>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -2037,59 +1027,48 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_generic(GemvParams p, int qua
 }
 
 // ---------------------------------------------------------------------------
-// host-side table construction
+// host side
 // ---------------------------------------------------------------------------
-static uint16_t f32_to_f16_bits(float f) {
-  return __half_as_ushort(__float2half_rn(f));  // host-side RNE conversion (hip_fp16.h)
-}
 
-static void build_tables(int mode, int quant_type, uint32_t tab[8], float *out_scale) {
-  for (int i = 0; i < 8; ++i) tab[i] = 0;
-  if (mode == kModeTab && quant_type == QZ_FP4) {
-    // 16-entry planes of the signed FP4 codebook x12: magnitudes {0, 1/16, 8, 12, 4, 6, 2, 3}
-    // are exact fp16 values with zero low bytes; codes 8..15 carry the sign (code 8 = -0.0)
-    const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t h = (uint32_t)hb[i & 7] | (i >= 8 ? 0x80u : 0u);
-      tab[4 + (i >> 2)] |= h << (8 * (i & 3));
-    }
-    *out_scale = 1.0f / 12.0f;
-    return;
-  }
-  if (mode == kModeFP4) {
-    // magnitudes x12 for codes 0..7: {0, 1/16, 8, 12, 4, 6, 2, 3}, fp16 high bytes (low bytes are 0)
-    const uint8_t hb[8] = {0x00, 0x2C, 0x48, 0x4A, 0x44, 0x46, 0x40, 0x42};
-    for (int i = 0; i < 8; ++i) tab[i >> 2] |= (uint32_t)hb[i] << (8 * (i & 3));
-    *out_scale = 1.0f / 12.0f;
-    return;
-  }
-  static const float nf4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
-                                -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
-                                0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
-                                0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-                                0.7229568362236023f, 1.0f};
-  (void)quant_type;
-  for (int i = 0; i < 16; ++i) {
-    const uint16_t h = f32_to_f16_bits(nf4[i]);
-    tab[i >> 2] |= (uint32_t)(h & 0xFF) << (8 * (i & 3));
-    tab[4 + (i >> 2)] |= (uint32_t)(h >> 8) << (8 * (i & 3));
-  }
-  *out_scale = 1.0f;
+// Measurement knobs of the launch geometry.  Read ONCE, when the library is loaded (a variable
+// set later changes nothing), and reported by qz_gemv_knobs() -- bench.py copies that into its
+// line's config, so a stray variable on a box cannot change what is measured unseen.
+struct Knobs {
+  int wide8;    // QZ_GEMV_WIDE8=0: long-K exact-code GEMVs on 4-wave workgroups (default: 8 waves, 256-B table)
+  int norm_r;   // QZ_GROUPED_NORM_R=1|2|4: rows per wave of the normed grouped launch (0 = geometry's)
+  int pair_r;   // QZ_PAIR_R=2|3|4|6|8: rows per wave of the pair launch (0 = geometry's)
+  int pair_wt;  // QZ_PAIR_WT=0: the persistent pair keeps the 16-copy exact table (default 1)
+  int pair_ps;  // QZ_PAIR_PS: 0 = one workgroup per block, 1..8 = workgroups per CU, >= 16 = the grid; -1 = default
+};
+static int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
+static Knobs read_knobs() {
+  Knobs k;
+  k.wide8 = env_int("QZ_GEMV_WIDE8", 1) != 0;
+  const int nr = env_int("QZ_GROUPED_NORM_R", 0);
+  k.norm_r = (nr == 1 || nr == 2 || nr == 4) ? nr : 0;
+  const int pr = env_int("QZ_PAIR_R", 0);
+  k.pair_r = (pr == 2 || pr == 3 || pr == 4 || pr == 6 || pr == 8) ? pr : 0;
+  k.pair_wt = env_int("QZ_PAIR_WT", 1) != 0;
+  k.pair_ps = env_int("QZ_PAIR_PS", -1);
+  return k;
+}
+static const Knobs g_knobs = read_knobs();   // at library load
 
-// Exact NF4 codes (CL) as fp16 byte planes: hi = fp16(c * 2^14) in `hi`, lo = fp16(c * 2^14 - hi)
-// in `lo` (the kernel's SGPR-built table, OPT & 2; the same values as g_byte_tab_nf4x)
-static void build_exact_planes(uint32_t hi[8], uint32_t lo[8]) {
-  for (int i = 0; i < 8; ++i) hi[i] = lo[i] = 0;
-  for (int i = 0; i < 16; ++i) {
-    const float c = kNF4Host[i] * (float)(1 << kNF4ExactShift);
-    const uint16_t h = f32_to_f16_bits(c);
-    const uint16_t l = f32_to_f16_bits(c - __half2float(__ushort_as_half(h)));
-    hi[i >> 2] |= (uint32_t)(h & 0xFF) << (8 * (i & 3));
-    hi[4 + (i >> 2)] |= (uint32_t)(h >> 8) << (8 * (i & 3));
-    lo[i >> 2] |= (uint32_t)(l & 0xFF) << (8 * (i & 3));
-    lo[4 + (i >> 2)] |= (uint32_t)(l >> 8) << (8 * (i & 3));
+// Compute units of the current device (hipDeviceGetAttribute), cached per device: the persistent
+// grids are sized in workgroups per CU.
+static int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v <= 0) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev].store(v, std::memory_order_relaxed);
   }
+  return v;
 }
 
 static int ilog2(long long v) {
@@ -2099,65 +1078,64 @@ static int ilog2(long long v) {
 }
 
 // Geometries choose_geometry can return: (R, WK) in {(4,1), (4,2), (2,1), (1,1), (1,2), (1,4)}.
-// two_steps(K, WK): every wave owns exactly two full K-steps (gemv_body OPT 8, the straight-line
-// form: step 2 issued right after the prologue barrier; profiles/r4_gemv_two_step.txt).  WK = 1
-// only: at K = 8192, WK = 2 (the Llama-3-70B q/k/v and o shapes, R = 4) hipcc gives the
-// straight-line body 259-278 VGPRs against 130 for the loop form -- one wave per SIMD
-// (profiles/r4_bench_70b_two_step_regression.txt)
+// two_steps(K, WK): every wave owns exactly two full K-steps (the straight-line TWO form;
+// profiles/r4_gemv_two_step.txt).  WK = 1 only: at K = 8192, WK = 2 (the Llama-3-70B q/k/v and o
+// shapes, R = 4) hipcc gave the straight-line body 259-278 VGPRs against 130 for the loop form --
+// one wave per SIMD (profiles/r4_bench_70b_two_step_regression.txt)
 static inline bool two_steps(int K, int WK, bool fs) { return fs && WK == 1 && K == 2 * 2048; }
 
-template <int MODE, bool DQ, int DT, bool FS, bool CL>
+template <bool DQ, int DT, bool FS, bool CL>
 static void launch_vec(const GemvParams &p, int R, int WK, hipStream_t s) {
   const int RG = 4 / WK;
   const unsigned grid = (unsigned)((p.M + R * RG - 1) / (R * RG));
-#define QZ_GV(RR, WW, OPT_) \
-  hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, RR, WW, 4, false, 0, FS, CL, false, 0, (WW == 1 ? OPT_ : 0)>), dim3(grid), \
-                     dim3(256), 0, s, p)
-#define QZ_GV_RW(OPT_)                        \
+#define QZ_GV(RR, WW, TWO_) \
+  hipLaunchKernelGGL((k_gemv_4bit<DQ, DT, RR, WW, 4, FS, CL, false, (WW == 1 && TWO_)>), dim3(grid), dim3(256), 0, s, p)
+#define QZ_GV_RW(TWO_)                        \
   do {                                        \
-    if (R == 4 && WK == 2) QZ_GV(4, 2, OPT_); \
-    else if (R == 4) QZ_GV(4, 1, OPT_);       \
-    else if (R == 2) QZ_GV(2, 1, OPT_);       \
-    else if (WK == 1) QZ_GV(1, 1, OPT_);      \
-    else if (WK == 2) QZ_GV(1, 2, OPT_);      \
-    else QZ_GV(1, 4, OPT_);                   \
+    if (R == 4 && WK == 2) QZ_GV(4, 2, TWO_); \
+    else if (R == 4) QZ_GV(4, 1, TWO_);       \
+    else if (R == 2) QZ_GV(2, 1, TWO_);       \
+    else if (WK == 1) QZ_GV(1, 1, TWO_);      \
+    else if (WK == 2) QZ_GV(1, 2, TWO_);      \
+    else QZ_GV(1, 4, TWO_);                   \
   } while (0)
   if constexpr (FS) {
-    if (two_steps(p.K, WK, true)) { QZ_GV_RW(8); return; }
+    if (two_steps(p.K, WK, true)) { QZ_GV_RW(true); return; }
   }
   // exact codes, K >= 14336 (down_proj: 7 or more K-steps per wave): 8-wave workgroups sharing one
   // 256-B-entry table (conflict-free, v_perm addresses): 4096 x 14336 8.92 -> 8.70 us, 8192 x 28672
   // (R = 4) 29.2 -> 25.5 us (profiles/r4_gemv_8wave_wide_table.txt); the per-row sums are the same
-  if constexpr (FS && CL && DT == QZ_DT_F16 && MODE == kModeTab) {
-    const char *w8 = getenv("QZ_GEMV_WIDE8");   // measurement knob (read per call): 0 = off
-    if (WK == 1 && (R == 2 || R == 4) && p.K >= 14336 && !(w8 && atoi(w8) == 0)) {
+  if constexpr (FS && CL && DT == QZ_DT_F16) {
+    if (WK == 1 && (R == 2 || R == 4) && p.K >= 14336 && g_knobs.wide8) {
       const unsigned g8 = (unsigned)((p.M + R * 8 - 1) / (R * 8));
-      if (R == 4) hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, 4, 1, 8, false, 0, FS, CL, true>), dim3(g8), dim3(512), 0, s, p);
-      else hipLaunchKernelGGL((k_gemv_4bit<MODE, DQ, DT, 2, 1, 8, false, 0, FS, CL, true>), dim3(g8), dim3(512), 0, s, p);
+      if (R == 4) hipLaunchKernelGGL((k_gemv_4bit<DQ, DT, 4, 1, 8, FS, CL, true, false>), dim3(g8), dim3(512), 0, s, p);
+      else hipLaunchKernelGGL((k_gemv_4bit<DQ, DT, 2, 1, 8, FS, CL, true, false>), dim3(g8), dim3(512), 0, s, p);
       return;
     }
   }
-  QZ_GV_RW(0);
+  QZ_GV_RW(false);
 #undef QZ_GV_RW
 #undef QZ_GV
 }
 
-template <int MODE, bool DQ, bool FS, bool CL>
+template <bool DQ, bool FS, bool CL>
 static int dispatch_dt(const GemvParams &p, int dtype, int R, int WK, hipStream_t s) {
   switch (dtype) {
-    case QZ_DT_F16: launch_vec<MODE, DQ, QZ_DT_F16, FS, CL>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_BF16: launch_vec<MODE, DQ, QZ_DT_BF16, FS, CL>(p, R, WK, s); return QZ_OK;
-    case QZ_DT_F32: launch_vec<MODE, DQ, QZ_DT_F32, FS, CL>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_F16: launch_vec<DQ, QZ_DT_F16, FS, CL>(p, R, WK, s); return QZ_OK;
+    case QZ_DT_BF16:
+      if constexpr (!CL) { launch_vec<DQ, QZ_DT_BF16, FS, false>(p, R, WK, s); return QZ_OK; }
+      break;
+    case QZ_DT_F32:
+      if constexpr (!CL) { launch_vec<DQ, QZ_DT_F32, FS, false>(p, R, WK, s); return QZ_OK; }
+      break;
   }
   return QZ_ERR_DTYPE;
 }
 
 template <bool CL>
 static int dispatch_tab(const GemvParams &p, int dtype, bool dq, bool fs, int R, int WK, hipStream_t s) {
-  if (fs) return dq ? dispatch_dt<kModeTab, true, true, CL>(p, dtype, R, WK, s)
-                    : dispatch_dt<kModeTab, false, true, CL>(p, dtype, R, WK, s);
-  return dq ? dispatch_dt<kModeTab, true, false, CL>(p, dtype, R, WK, s)
-            : dispatch_dt<kModeTab, false, false, CL>(p, dtype, R, WK, s);
+  if (fs) return dq ? dispatch_dt<true, true, CL>(p, dtype, R, WK, s) : dispatch_dt<false, true, CL>(p, dtype, R, WK, s);
+  return dq ? dispatch_dt<true, false, CL>(p, dtype, R, WK, s) : dispatch_dt<false, false, CL>(p, dtype, R, WK, s);
 }
 
 }  // namespace qz
@@ -2165,7 +1143,7 @@ static int dispatch_tab(const GemvParams &p, int dtype, bool dq, bool fs, int R,
 using namespace qz;
 
 // Geometry (WK = waves along K, R = rows per wave) for the byte-table decode,
-// from the measured shape sweep in DESIGN.md section 4.1 (scripts/gpu_sessions/run24.sh):
+// from the measured shape sweep in DESIGN.md section 4.1:
 //  * >= 64 Mi weights (gate/up groups, 8192x28672, ...): R=4 -- more bytes in
 //    flight per wave and fewer x/scale loads per weight byte;
 //  * smaller: R=2;
@@ -2201,24 +1179,14 @@ static bool full_steps(int K, int blocksize, int blocksize2, bool dq, long long 
   return !dq || blocksize2 % step_blocks == 0;
 }
 
-// Decode tables for the byte-table kernel: the 16-entry codebook as fp16 byte
-// planes (a runtime `lut` is converted in kernel, so its planes stay zero).
-// Exact codes (CL): the built-in NF4 table holds code * 2^14 as hi + lo.
+// The byte table a launch uses and the scale it undoes on the output.  bf16 / fp32 x: the NF4 or
+// FP4 x12 code table of that dtype; fp16 x: fp16-rounded NF4 (tabsel 0), FP4 x12 (1) or the exact
+// NF4 codes x 2^14 (CL, 2).  A runtime codebook is converted in kernel (out_scale set there).
 static void set_tables(int quant_type, const float *lut, bool cl, int dtype, GemvParams *p) {
-  build_tables(kModeTab, lut ? QZ_NF4 : quant_type, p->tab, &p->out_scale);
-  if (dtype == QZ_DT_BF16 || dtype == QZ_DT_F32) {  // bf16 / fp32 code tables: NF4 codes, FP4 x12
-    const bool fp4 = !lut && quant_type == QZ_FP4;
-    p->tabsel = fp4 ? 1 : 0;
-    p->out_scale = fp4 ? 1.0f / 12.0f : 1.0f;
-    return;
-  }
-  p->tabsel = (!lut && quant_type == QZ_FP4) ? 1 : (cl ? 2 : 0);
-  for (int i = 0; i < 8; ++i) p->tab_lo[i] = 0;
-  if (lut) p->out_scale = 1.0f;
-  else if (cl) {
-    p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
-    build_exact_planes(p->tab, p->tab_lo);
-  }
+  const bool fp4 = !lut && quant_type == QZ_FP4;
+  p->tabsel = fp4 ? 1 : (cl && dtype == QZ_DT_F16 ? 2 : 0);
+  p->out_scale = fp4 ? 1.0f / 12.0f : 1.0f;
+  if (dtype == QZ_DT_F16 && cl && !lut) p->out_scale = 1.0f / (float)(1 << kNF4ExactShift);
 }
 
 // Exact codes: a runtime codebook is always decoded exactly (the reference
@@ -2256,13 +1224,11 @@ static int make_params(int M, int K, const void *x, int dtype, const unsigned ch
   p->K = K;
   p->bs_log2 = bsl;
   p->bs2_log2 = bs2l;
+  p->out_scale = 1.0f;
+  p->tabsel = 0;
   p->nw = nullptr;
   p->eps = 0.0f;
   p->res = nullptr;
-  p->pf = nullptr;
-  p->pf_row_bytes = 0;
-  p->pf_rows = 0;
-  p->pf_chunks = 0;
   *vec_ok = K > 0 && (K % 32) == 0 && blocksize >= 32 && (reinterpret_cast<uintptr_t>(B) % 16) == 0 &&
             (reinterpret_cast<uintptr_t>(x) % 16) == 0 &&
             (long long)M * K + 2LL * 1024 < (1LL << 32) &&            // 32-bit element offsets
@@ -2283,8 +1249,8 @@ static int gemv_impl(int M, int K, const void *x, int dtype, const unsigned char
   if (M == 0) return QZ_OK;
   const bool dq = qabsmax != nullptr;
   hipStream_t s = (hipStream_t)stream;
-  // bf16 x always decodes with bf16 hi + lo codes (~2^-16) and fp32 x with fp32 codes: the
-  // exact-code (CL) variant is the fp16-activation option only
+  // bf16 x always decodes with bf16 hi + lo codes and fp32 x with fp32 codes: the exact-code (CL)
+  // variant is the fp16-activation option only
   const bool cl = exact_codes(quant_type, lut) && dtype == QZ_DT_F16;
   quant_type &= ~QZ_EXACT_CODES;
 
@@ -2375,14 +1341,9 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   }
   int R, WK;
   choose_geometry((int)total_m, K, dtype, &R, &WK);
-  // QZ_GROUPED_NORM_R (measurement knob, read once): rows per wave of the fused pre-norm launch
-  // (1, 2, 4) where the geometry keeps whole rows per wave (WK = 1: the same per-row sums)
-  static const int norm_r = [] {
-    const char *e = getenv("QZ_GROUPED_NORM_R");
-    const int v = e ? atoi(e) : 0;
-    return v == 1 || v == 2 || v == 4 ? v : 0;
-  }();
-  if (nw && norm_r && WK == 1) R = norm_r;
+  // QZ_GROUPED_NORM_R (knob): rows per wave of the fused pre-norm launch where the geometry keeps
+  // whole rows per wave (WK = 1: the same per-row sums)
+  if (nw && g_knobs.norm_r && WK == 1) R = g_knobs.norm_r;
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -2401,114 +1362,41 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;
   const bool two = two_steps(K, WK, all_fs || nw);
-#define QZ_GR1(DQ_, DT_, RR, WW, FS_, OPT_)                                                                    \
-  do {                                                                                                      \
-    if (cl) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, true, false, OPT_>),   \
-                               dim3(blocks), dim3(256), 0, s, g);                                           \
-    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, FS_, false, false, OPT_>),     \
-                            dim3(blocks), dim3(256), 0, s, g);                                              \
+  const size_t lds = nw ? (size_t)K * 2 : 0;
+#define QZ_GR1(DQ_, DT_, RR, WW, FS_, CL_, NRM_)                                                            \
+  do {                                                                                                    \
+    if (FS_ && two && WW == 1)                                                                            \
+      hipLaunchKernelGGL((k_gemv_4bit_grouped<DQ_, DT_, RR, WW, FS_, CL_, NRM_, (FS_ && WW == 1)>), dim3(blocks), \
+                         dim3(256), lds, s, g);                                                           \
+    else hipLaunchKernelGGL((k_gemv_4bit_grouped<DQ_, DT_, RR, WW, FS_, CL_, NRM_, false>), dim3(blocks),      \
+                            dim3(256), lds, s, g);                                                        \
   } while (0)
-#define QZ_GR(DQ_, DT_, RR, WW, FS_)                                 \
-  do {                                                               \
-    if (FS_ && two) QZ_GR1(DQ_, DT_, RR, WW, FS_, (FS_ && WW == 1 ? 8 : 0));    \
-    else QZ_GR1(DQ_, DT_, RR, WW, FS_, 0);                           \
+#define QZ_GR_RW(DQ_, DT_, FS_, CL_, NRM_)                                                                  \
+  do {                                                                                                    \
+    if (R == 4 && WK == 2) QZ_GR1(DQ_, DT_, 4, 2, FS_, CL_, NRM_);                                        \
+    else if (R == 4) QZ_GR1(DQ_, DT_, 4, 1, FS_, CL_, NRM_);                                              \
+    else if (R == 2) QZ_GR1(DQ_, DT_, 2, 1, FS_, CL_, NRM_);                                              \
+    else if (WK == 1) QZ_GR1(DQ_, DT_, 1, 1, FS_, CL_, NRM_);                                             \
+    else if (WK == 2) QZ_GR1(DQ_, DT_, 1, 2, FS_, CL_, NRM_);                                             \
+    else QZ_GR1(DQ_, DT_, 1, 4, FS_, CL_, NRM_);                                                          \
   } while (0)
-#define QZ_GR_RW(DQ_, DT_, FS_)                                      \
-  do {                                                               \
-    if (R == 4 && WK == 2) QZ_GR(DQ_, DT_, 4, 2, FS_);               \
-    else if (R == 4) QZ_GR(DQ_, DT_, 4, 1, FS_);                     \
-    else if (R == 2) QZ_GR(DQ_, DT_, 2, 1, FS_);                     \
-    else if (WK == 1) QZ_GR(DQ_, DT_, 1, 1, FS_);                    \
-    else if (WK == 2) QZ_GR(DQ_, DT_, 1, 2, FS_);                    \
-    else QZ_GR(DQ_, DT_, 1, 4, FS_);                                 \
+#define QZ_GR_DT(DQ_, FS_)                                                                                  \
+  do {                                                                                                    \
+    if (dtype == QZ_DT_F16) { if (cl) QZ_GR_RW(DQ_, QZ_DT_F16, FS_, true, false); else QZ_GR_RW(DQ_, QZ_DT_F16, FS_, false, false); } \
+    else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_, false, false);                         \
+    else QZ_GR_RW(DQ_, QZ_DT_F32, FS_, false, false);                                                    \
   } while (0)
-#define QZ_GR_DT(DQ_, FS_)                                           \
-  do {                                                               \
-    if (dtype == QZ_DT_F16) QZ_GR_RW(DQ_, QZ_DT_F16, FS_);           \
-    else if (dtype == QZ_DT_BF16) QZ_GR_RW(DQ_, QZ_DT_BF16, FS_);    \
-    else QZ_GR_RW(DQ_, QZ_DT_F32, FS_);                              \
-  } while (0)
-  // QZ_GROUPED_EARLY=1 (measurement knob, read per call): the normed two-step launch issues its second
-  // K-step before the prologue barriers (OPT 1 | 8) instead of after them
-  const char *gee = getenv("QZ_GROUPED_EARLY");
-  const bool g_early = gee && atoi(gee) == 1;
-#define QZ_GN(DQ_, DT_, RR, WW, CL_)                                                                          \
-  do {                                                                                                        \
-    if (two && g_early && WW == 1)                                                                            \
-      hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, (WW == 1 ? 9 : 0)>), dim3(blocks), \
-                         dim3(256), (size_t)K * 2, s, g);                                                     \
-    else if (two) hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true, (WW == 1 ? 8 : 0)>), \
-                                dim3(blocks), dim3(256), (size_t)K * 2, s, g);                                \
-    else hipLaunchKernelGGL((k_gemv_4bit_grouped<kModeTab, DQ_, DT_, RR, WW, true, CL_, true>), dim3(blocks),  \
-                            dim3(256), (size_t)K * 2, s, g);                                                  \
-  } while (0)
-#define QZ_GN_RW(DQ_, DT_, CL_)                                      \
-  do {                                                               \
-    if (R == 4 && WK == 2) QZ_GN(DQ_, DT_, 4, 2, CL_);               \
-    else if (R == 4) QZ_GN(DQ_, DT_, 4, 1, CL_);                     \
-    else if (R == 2) QZ_GN(DQ_, DT_, 2, 1, CL_);                     \
-    else if (WK == 1) QZ_GN(DQ_, DT_, 1, 1, CL_);                    \
-    else if (WK == 2) QZ_GN(DQ_, DT_, 1, 2, CL_);                    \
-    else QZ_GN(DQ_, DT_, 1, 4, CL_);                                 \
-  } while (0)
-  // QZ_GROUPED_PS (measurement knob, read per call): persistent workgroups for the two-step grouped
-  // launch with the fused norm: 1..8 per CU, >= 16 the grid; QZ_GROUPED_PS_R rows per wave (1, 2, 4)
-  // and QZ_GROUPED_WT=1 the 256-B-entry exact-code table
-  if (nw && two && WK == 1) {
-    const char *gpe = getenv("QZ_GROUPED_PS");
-    const int gps = gpe ? atoi(gpe) : 0;
-    if (gps > 0) {
-      int Rg = R;
-      if (const char *gre = getenv("QZ_GROUPED_PS_R")) {
-        const int v = atoi(gre);
-        if (v == 1 || v == 2 || v == 4) Rg = v;
-      }
-      GemvGroup g2 = g;
-      int gb = 0;
-      for (int i = 0; i < nseg; ++i) {
-        g2.start[i] = gb;
-        gb += (g2.seg[i].M + 4 * Rg - 1) / (4 * Rg);
-      }
-      for (int i = nseg; i < kMaxSeg; ++i) g2.start[i] = gb;
-      g2.total = gb;
-      const unsigned ggrid = (unsigned)(gps <= 8 ? 256 * gps : gps);
-      const char *gwe = getenv("QZ_GROUPED_WT");
-      const bool gwt = gwe && atoi(gwe) == 1 && cl && dtype == QZ_DT_F16;
-      if ((int)ggrid < gb) {
-        const size_t lds = (size_t)K * 2;
-#define QZ_GP(DQ_, DT_, RR)                                                                                 \
-  do {                                                                                                      \
-    if (gwt) launch_grouped_ps<DQ_, DT_, RR, true, true>(ggrid, lds, s, g2);                                \
-    else if (cl) launch_grouped_ps<DQ_, DT_, RR, true, false>(ggrid, lds, s, g2);                           \
-    else launch_grouped_ps<DQ_, DT_, RR, false, false>(ggrid, lds, s, g2);                                  \
-  } while (0)
-#define QZ_GP_R(DQ_, DT_)                                                                                   \
-  do {                                                                                                      \
-    if (Rg == 4) QZ_GP(DQ_, DT_, 4); else if (Rg == 2) QZ_GP(DQ_, DT_, 2); else QZ_GP(DQ_, DT_, 1);        \
-  } while (0)
-        if (dtype == QZ_DT_F16) { if (dq) QZ_GP_R(true, QZ_DT_F16); else QZ_GP_R(false, QZ_DT_F16); }
-        else { if (dq) QZ_GP_R(true, QZ_DT_BF16); else QZ_GP_R(false, QZ_DT_BF16); }
-#undef QZ_GP_R
-#undef QZ_GP
-        QZ_LAUNCH_CHECK();
-        return QZ_OK;
-      }
-    }
-  }
   if (nw) {
     if (dtype == QZ_DT_F16) {
-      if (dq) { if (cl) QZ_GN_RW(true, QZ_DT_F16, true); else QZ_GN_RW(true, QZ_DT_F16, false); }
-      else { if (cl) QZ_GN_RW(false, QZ_DT_F16, true); else QZ_GN_RW(false, QZ_DT_F16, false); }
+      if (dq) { if (cl) QZ_GR_RW(true, QZ_DT_F16, true, true, true); else QZ_GR_RW(true, QZ_DT_F16, true, false, true); }
+      else { if (cl) QZ_GR_RW(false, QZ_DT_F16, true, true, true); else QZ_GR_RW(false, QZ_DT_F16, true, false, true); }
     } else {
-      if (dq) QZ_GN_RW(true, QZ_DT_BF16, false); else QZ_GN_RW(false, QZ_DT_BF16, false);
+      if (dq) QZ_GR_RW(true, QZ_DT_BF16, true, false, true); else QZ_GR_RW(false, QZ_DT_BF16, true, false, true);
     }
   } else if (all_fs) { if (dq) QZ_GR_DT(true, true); else QZ_GR_DT(false, true); }
   else { if (dq) QZ_GR_DT(true, false); else QZ_GR_DT(false, false); }
-#undef QZ_GN_RW
-#undef QZ_GN
 #undef QZ_GR_DT
 #undef QZ_GR_RW
-#undef QZ_GR
 #undef QZ_GR1
   QZ_LAUNCH_CHECK();
   return QZ_OK;
@@ -2524,6 +1412,14 @@ extern "C" int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *seg
                                             const void *norm_weight, float eps, void *stream) {
   if (!norm_weight || !x) return QZ_ERR_ARG;
   return gemv_grouped_impl(nseg, segs, K, x, dtype, quant_type, blocksize, blocksize2, lut, norm_weight, eps, stream);
+}
+
+// the persistent exact-code pair on the 256-B-entry table (64 KiB: 32 bank-private copies of each 8-B
+// entry, v_perm addresses), 2 workgroups per CU
+template <bool DQ, int DT, int R, bool CL, bool NRM>
+static void launch_pair_wt(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
+  if constexpr (CL && NRM && DT == QZ_DT_F16 && (R == 2 || R == 4))
+    hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, true, true, true>), dim3(grid), dim3(256), lds, s, g);
 }
 
 // LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (modeling_llama.py:175, hidden_act "silu") in one
@@ -2561,14 +1457,7 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
   if (WK != 1) return QZ_ERR_SHAPE;
-  // QZ_PAIR_R (measurement knob, read once): rows per wave for the pair launch (2, 3, 4, 6, 8); the per-row
-  // sums do not depend on R, so neither do the bits
-  static const int pair_r = [] {
-    const char *e = getenv("QZ_PAIR_R");
-    const int v = e ? atoi(e) : 0;
-    return v == 2 || v == 3 || v == 4 || v == 6 || v == 8 ? v : 0;
-  }();
-  if (pair_r) R = pair_r;
+  if (g_knobs.pair_r) R = g_knobs.pair_r;   // knob; the per-row sums do not depend on R
   const int blocks = (M + 2 * R - 1) / (2 * R);
   if (norm_weight && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
   for (int i = 2; i < kMaxSeg; ++i) g.start[i] = 0;
@@ -2580,24 +1469,20 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   // profiles/r4_pair_persistent.txt: 14336 rows 19.5 -> 16.4 us, 7168 rows 13.9 -> 10.4 us, the
   // N = 4 / 8 shards 8.9 -> 7.4 and 7.9 -> 6.3 us; without the norm the one-block-per-workgroup
   // launch stays faster).  Grid: 3 workgroups per CU (what the 43 KiB LDS image admits), the best
-  // or within 4 % of the best of 2 / 3 / 4 per CU and of blocks / 2 at every shape.  QZ_PAIR_PS
-  // (measurement knob, read per call) overrides: 1..8 = workgroups per CU, >= 16 = the grid, 0 = one
-  // workgroup per block
+  // or within 4 % of the best of 2 / 3 / 4 per CU and of blocks / 2 at every shape.
   // With exact codes and R = 2 / 4 the persistent pair takes the 256-B-entry table (64 KiB: 32
   // bank-private copies of each 8-B entry, one v_perm per address, no bank conflicts) at 2
   // workgroups per CU: 16.2-16.8 -> 15.1 us for 14336 rows, 10.8 -> 10.6 for 7168
-  // (profiles/r4_pair_persistent_wide_table.txt); QZ_PAIR_WT=0 (knob, read per call) keeps the 16-copy table
-  const char *wte = getenv("QZ_PAIR_WT");
-  // (from 3 blocks per workgroup on: at the N = 4 shard, 896 blocks, the 16-copy table at 3 per CU is
-  // 3 % faster)
-  const bool wt_ok = cl && norm_weight && (R == 2 || R == 4) && blocks >= 3 * 512 && !(wte && atoi(wte) == 0);
-  const char *pse = getenv("QZ_PAIR_PS");
+  // (profiles/r4_pair_persistent_wide_table.txt), from 3 blocks per workgroup on (at the N = 4
+  // shard, 896 blocks, the 16-copy table at 3 per CU is 3 % faster)
+  const int cus = device_cus();
+  const bool wt_ok = cl && norm_weight && (R == 2 || R == 4) && blocks >= 3 * 2 * cus && g_knobs.pair_wt;
   int pgrid_i = 0;
-  if (pse) {
-    const int ps = atoi(pse);
-    pgrid_i = ps <= 0 ? 0 : ps <= 8 ? 256 * ps : ps;
+  if (g_knobs.pair_ps >= 0) {
+    const int ps = g_knobs.pair_ps;
+    pgrid_i = ps <= 0 ? 0 : ps <= 8 ? cus * ps : ps;
   } else if (norm_weight) {
-    pgrid_i = (wt_ok ? 2 : 3) * 256;
+    pgrid_i = (wt_ok ? 2 : 3) * cus;
   }
   const unsigned pgrid = (unsigned)max(pgrid_i, 1);
   const bool persist = two && pgrid_i > 0 && pgrid_i < blocks;
@@ -2605,24 +1490,23 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
 #define QZ_PS(DQ_, DT_, RR, CL_, NRM_)                                                                               \
   do {                                                                                                              \
     if (pair_wt) launch_pair_wt<DQ_, DT_, RR, CL_, NRM_>(pgrid, lds, s, g);                                        \
-    else if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8, true>), dim3(pgrid), \
-                                    dim3(256), lds, s, g);                                                          \
-    else if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_, 8>), dim3(blocks),    \
-                                     dim3(256), lds, s, g);                                                         \
-    else hipLaunchKernelGGL((k_gemv_4bit_pair<kModeTab, DQ_, DT_, RR, true, CL_, NRM_>), dim3(blocks), dim3(256), lds, \
-                            s, g);                                                                                  \
+    else if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, true, true>), dim3(pgrid),      \
+                                         dim3(256), lds, s, g);                                                     \
+    else if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, true>), dim3(blocks), dim3(256),    \
+                                     lds, s, g);                                                                    \
+    else hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, false>), dim3(blocks), dim3(256), lds, s, g); \
   } while (0)
-#define QZ_PS_R(DQ_, DT_, CL_, NRM_)           \
-  do {                                          \
-    if (R == 4) QZ_PS(DQ_, DT_, 4, CL_, NRM_);  \
-    else if (R == 8) QZ_PS(DQ_, DT_, 8, CL_, NRM_);  \
-    else if (R == 6) QZ_PS(DQ_, DT_, 6, CL_, NRM_);  \
-    else if (R == 3) QZ_PS(DQ_, DT_, 3, CL_, NRM_);  \
-    else if (R == 1) QZ_PS(DQ_, DT_, 1, CL_, NRM_);  \
-    else QZ_PS(DQ_, DT_, 2, CL_, NRM_);         \
+#define QZ_PS_R(DQ_, DT_, CL_, NRM_)                  \
+  do {                                                \
+    if (R == 4) QZ_PS(DQ_, DT_, 4, CL_, NRM_);        \
+    else if (R == 8) QZ_PS(DQ_, DT_, 8, CL_, NRM_);   \
+    else if (R == 6) QZ_PS(DQ_, DT_, 6, CL_, NRM_);   \
+    else if (R == 3) QZ_PS(DQ_, DT_, 3, CL_, NRM_);   \
+    else if (R == 1) QZ_PS(DQ_, DT_, 1, CL_, NRM_);   \
+    else QZ_PS(DQ_, DT_, 2, CL_, NRM_);               \
   } while (0)
-#define QZ_PS_N(DQ_, DT_, CL_)                                                      \
-  do {                                                                              \
+#define QZ_PS_N(DQ_, DT_, CL_)                                                         \
+  do {                                                                                 \
     if (norm_weight) QZ_PS_R(DQ_, DT_, CL_, true); else QZ_PS_R(DQ_, DT_, CL_, false); \
   } while (0)
   if (dtype == QZ_DT_F16) {
@@ -2636,4 +1520,16 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
 #undef QZ_PS
   QZ_LAUNCH_CHECK();
   return QZ_OK;
+}
+
+// The launch-geometry knobs in effect (read once at library load) as a JSON object, for the bench
+// line's config.  Returns the length written (excluding the NUL), or the length needed if n is too small.
+extern "C" int qz_gemv_knobs(char *buf, int n) {
+  char tmp[256];
+  const int len = snprintf(tmp, sizeof(tmp),
+                           "{\"QZ_GEMV_WIDE8\": %d, \"QZ_GROUPED_NORM_R\": %d, \"QZ_PAIR_R\": %d, \"QZ_PAIR_WT\": %d, "
+                           "\"QZ_PAIR_PS\": %d, \"cus\": %d}",
+                           g_knobs.wide8, g_knobs.norm_r, g_knobs.pair_r, g_knobs.pair_wt, g_knobs.pair_ps, device_cus());
+  if (buf && n > len) memcpy(buf, tmp, (size_t)len + 1);
+  return len;
 }

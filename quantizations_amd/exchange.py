@@ -139,30 +139,41 @@ class OneShotAllGather:
                         ok = False
         return bool(_vote(ok and not self.failed(), dist.ReduceOp.MIN, self.group, self.device))
 
-    def warm_graph(self, replays: int = 3) -> None:
+    def warm_graph(self, replays: int = 3) -> bool:
         """Capture and replay a throwaway HIP graph of one call per protocol (collective: every
         rank calls it).  Measured with two processes on one MI355X: the FIRST graph a process
         captures runs its exchanges at ~28 us per call for every replay, whatever the protocol
         or payload, and every later graph at 3.5-4 us; a throwaway graph first removes it
-        (`profiles/r4_exchange_first_graph.txt`).  Run before the decode graph is captured."""
-        n = 256
-        x = torch.zeros(n, device=self.device, dtype=torch.float16)
-        out = torch.empty(self.world * n, device=self.device, dtype=torch.float16)
-        s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            self(out, x, 1)
-            self(out, x, 2)
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self(out, x, 1)
-            self(out, x, 2)
-        for _ in range(replays):
-            g.replay()
-        torch.cuda.synchronize(self.device)
-        del g
+        (`profiles/r4_exchange_first_graph.txt`).  Run before the decode graph is captured.
+        Returns the MIN vote of every rank's success (a local failure is voted on, never raised
+        on one rank while the others go on): False means no rank may use this gatherer."""
+        ok = True
+        try:
+            n = 256
+            x = torch.zeros(n, device=self.device, dtype=torch.float16)
+            out = torch.empty(self.world * n, device=self.device, dtype=torch.float16)
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self(out, x, 1)
+                self(out, x, 2)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self(out, x, 1)
+                self(out, x, 2)
+            for _ in range(replays):
+                g.replay()
+            torch.cuda.synchronize(self.device)
+            del g
+        except Exception:  # noqa: BLE001 -- reported by the vote below
+            ok = False
+        try:
+            ok = ok and not self.failed()
+        except Exception:  # noqa: BLE001
+            ok = False
+        return bool(_vote(ok, dist.ReduceOp.MIN, self.group, self.device))
 
     def close(self) -> None:
         for p in self._opened:

@@ -141,7 +141,8 @@ class RowShardedLinear4bit(nn.Module):
         (qz_gemv_4bit_residual: the same bits as the unsharded layer's fused epilogue), and the
         rows are gathered afterwards.  Anything else: the two-op form."""
         if (self._local_matmul is None and self.gather and x.is_cuda and x.numel() == x.shape[-1]
-                and residual.dtype == x.dtype and residual.is_contiguous() and residual.numel() == self.out_features
+                and residual.dtype == x.dtype and residual.device == x.device and residual.is_contiguous()
+                and residual.numel() == self.out_features and residual.shape[:-1] == x.shape[:-1]
                 and self.__dict__.get("_qz_group") is None):
             from .core import gemv_4bit
             rows = residual.reshape(-1)[self.r0:self.r1]

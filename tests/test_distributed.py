@@ -195,10 +195,12 @@ def _tp_hook(x, mod):
     return y.to(x.dtype)
 
 
-def _tiny_llama_4bit():
+def _tiny_llama_4bit(world: int = 2):
     """A tiny fp32 Llama whose decoder linears are Linear4bit layers built from
     ORACLE-quantised weights (layer 0 NF4, layer 1 FP4, double quant), plus the
-    unsharded reference model holding the oracle's dequantised weights."""
+    unsharded reference model holding the oracle's dequantised weights.  world > 2: a 512-wide
+    model with 8 query and 8 kv heads, so the Megatron pairing can split heads and whole scale
+    blocks over up to 8 ranks."""
     import copy
 
     import oracle
@@ -207,8 +209,10 @@ def _tiny_llama_4bit():
     from quantizations_amd.core import Params4bit, QuantState, create_dynamic_map, get_4bit_type
     from quantizations_amd.modules import Linear4bit
 
-    cfg = LlamaConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
-                      num_key_value_heads=2, vocab_size=97)
+    # world > 2: widths whose column shards keep whole 64-element scale blocks at 8 ranks
+    hidden, inter, heads, kv = (128, 256, 4, 2) if world <= 2 else (512, 512, 8, 8)
+    cfg = LlamaConfig(hidden_size=hidden, intermediate_size=inter, num_hidden_layers=2, num_attention_heads=heads,
+                      num_key_value_heads=kv, vocab_size=97)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg).float().eval()
     ref = copy.deepcopy(model)
@@ -311,7 +315,7 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch, layer_ops="none")
         import bench
         from quantizations_amd.parallel import RowShardedLinear4bit
 
-        cfg, model, ref = _tiny_llama_4bit()
+        cfg, model, ref = _tiny_llama_4bit(world)
         n_groups, n_ops = bench.prepare_decode_model(model, rank, world, True, tp_mode, fuse=True,
                                                      layer_ops=layer_ops, local_matmul=_tp_hook)
         if layer_ops != "none":
@@ -353,17 +357,18 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch, layer_ops="none")
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("tp_mode,batch,layer_ops", [("gather", 1, "none"), ("pair", 2, "none"), ("gather", 1, "all"),
-                                                    ("pair", 1, "all")])
-def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops):
-    """bench.py --gpus 2 exactly as the driver runs it, on gloo world 2 with the
+@pytest.mark.parametrize("tp_mode,batch,layer_ops,world", [
+    ("gather", 1, "none", 2), ("pair", 2, "none", 2), ("gather", 1, "all", 2), ("pair", 1, "all", 2),
+    # config #5's rank counts: the row split + exchange at 4 and 8 ranks, the weak-scaling extra at 8
+    ("gather", 1, "all", 4), ("gather", 1, "all", 8), ("pair", 8, "none", 8)])
+def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops, world):
+    """bench.py --gpus N exactly as the driver runs it, on gloo world N (2, 4, 8) with the
     oracle as each shard's local product: the default strong-scaling layout
     (one bs=1 stream, every Linear4bit row-split + all-gather) and the
     weak-scaling extra (two streams, Megatron pairing).  The greedy tokens of 7
     decode steps equal the unsharded model's on every rank.  layer_ops "all": the
     fused decoder layer on the shards (absorbed norms, the sharded SiLU pair, the
     residual epilogues), as bench.py sets it up for N > 1."""
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,4 +1,4 @@
-"""The one-shot all-gather's host logic on CPU (gloo world 2): the test-only shared-memory
+"""The one-shot all-gather's host logic on CPU (gloo world 2, 4 and 8 -- config #5's ranks): the test-only shared-memory
 rehearsal of comm.hip's protocol (tests/exchange_emulation.py) returns exactly what
 dist.all_gather_into_tensor returns -- rank-major shard placement, both slot parities,
 payloads from 16 B to the slot size -- and, as the `gatherer` of the row-split model,
@@ -46,8 +46,8 @@ def _placement_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_oneshot_protocol_placement_and_parity():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_oneshot_protocol_placement_and_parity(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,7 +74,7 @@ def _model_worker(rank, world, port, q):
         from quantizations_amd.integration import fuse_projection_groups
         from quantizations_amd.parallel import shard_model_linear4bit
 
-        cfg, model, ref = _tiny_llama_4bit()
+        cfg, model, ref = _tiny_llama_4bit(world)
         ag = ShmAllGather(slot_bytes=1024, tag=f"m{port}")
         shard_model_linear4bit(model, rank, world, local_matmul=_tp_hook, gatherer=ag)
         n_groups = fuse_projection_groups(model)
@@ -88,8 +88,8 @@ def _model_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_row_split_model_through_oneshot_gatherer():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_row_split_model_through_oneshot_gatherer(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,6 +1,6 @@
 """GPU: the one-shot all-gather (comm.hip k_allgather_oneshot through exchange.OneShotAllGather)
-between two processes -- two ranks on the box's one MI355X, each mapping the other's
-uncached exchange buffer through a hipIpc handle (on an 8-GPU node the same code maps
+between 2, 4 and 8 processes -- ranks on the box's one MI355X, each mapping the others'
+uncached exchange buffers through a hipIpc handle (on an 8-GPU node the same code maps
 the peers' buffers over xGMI).  Every call's rank-major result equals the concatenation
 of both ranks' shards, over payload sizes from 16 B to the slot size, both slot parities,
 both protocols (flags, tagged granules) interleaved, eager launches and a HIP-graph replay;
@@ -73,8 +73,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_oneshot_allgather_two_processes_one_gpu():
-    world = 2
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_oneshot_allgather_processes_one_gpu(world):
+    """world 8 is config #5's rank count: 8 processes on the one MI355X, each mapping the 7
+    others' buffers (the 8-rank granule regions, the epoch ticket at 8 writers)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -84,7 +87,7 @@ def test_oneshot_allgather_two_processes_one_gpu():
     for p in procs:
         p.start()
     try:
-        res = [q.get(timeout=150) for _ in range(world)]
+        res = [q.get(timeout=360) for _ in range(world)]
     finally:
         for p in procs:
             p.join(timeout=30)

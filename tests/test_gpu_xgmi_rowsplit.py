@@ -23,13 +23,14 @@ from test_distributed import _free_port
 pytestmark = pytest.mark.gpu
 
 
-def _model(dev):
+def _model(dev, world=2):
     from transformers import LlamaConfig, LlamaForCausalLM
 
     from quantizations_amd.integration import replace_with_bnb_linear
 
+    # 8 kv heads from 4 ranks on, so the Megatron pairing splits them
     cfg = LlamaConfig(hidden_size=512, intermediate_size=1024, num_hidden_layers=2, num_attention_heads=8,
-                      num_key_value_heads=4, vocab_size=1024, max_position_embeddings=256)
+                      num_key_value_heads=4 if world <= 2 else 8, vocab_size=1024, max_position_embeddings=256)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg).half().to(dev).eval()
     replace_with_bnb_linear(model, quant_type="nf4", compute_dtype=torch.float32)
@@ -55,7 +56,7 @@ def _work(rank, world, port, q, layout):
         from quantizations_amd.parallel import RowShardedLinear4bit, apply_tensor_parallel, shard_model_linear4bit
 
         dev = torch.device("cuda", 0)
-        cfg, model = _model(dev)
+        cfg, model = _model(dev, world)
         ref = copy.deepcopy(model)
         ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
         if layout.startswith("gather"):
@@ -85,13 +86,16 @@ def _work(rank, world, port, q, layout):
             decode_rel = ((a1 - b1).norm() / b1.norm()).item()
         torch.cuda.synchronize()
         dist.barrier()
-        # bench.py's decode loop, HIP-graph captured, at world 2
+        # bench.py's decode loop, HIP-graph captured, at world N; the unsharded model's greedy decode
+        # (the same kernels on all rows) on this process for comparison
         _, hist = bench.decode_bench_graph(model, cfg, steps=6, warmup=2, prompt_len=8, world=world, batch=1)
         hist = hist.cpu()
+        _, ref_hist = bench.decode_bench_graph(ref, cfg, steps=6, warmup=2, prompt_len=8, world=1, batch=1)
+        same_as_unsharded = bool(torch.equal(hist, ref_hist.cpu()))
         allh = [None] * world
         dist.all_gather_object(allh, hist)
         q0 = model.model.layers[0].self_attn.q_proj
-        q.put((rank, n_groups, prefill_rel, decode_rel, bool(torch.equal(allh[0], allh[1])),
+        q.put((rank, n_groups, prefill_rel, decode_rel, all(torch.equal(allh[0], h) for h in allh), same_as_unsharded,
                int((hist[:, 8:16] != 0).sum()), ag.failed_anywhere(), isinstance(q0, RowShardedLinear4bit),
                q0.r1 - q0.r0, q0.r0, fused_ok))
         dist.barrier()
@@ -100,9 +104,13 @@ def _work(rank, world, port, q, layout):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["gather", "pair", "gather-fused", "pair-fused"])
-def test_rowsplit_world2_oneshot_on_gpu(layout):
-    world = 2
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("layout,world", [("gather", 2), ("pair", 2), ("gather-fused", 2), ("pair-fused", 2),
+                                          ("gather-fused", 4), ("gather-fused", 8), ("pair-fused", 8)])
+def test_rowsplit_oneshot_on_gpu(layout, world):
+    """world 8: config #5's layout with 8 processes on the one MI355X (each mapping the 7 others'
+    exchange buffers); gather layouts decode exactly the unsharded model's greedy tokens (a shard's
+    rows are summed in the same order as the unsharded launch's)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -112,7 +120,7 @@ def test_rowsplit_world2_oneshot_on_gpu(layout):
     for p in procs:
         p.start()
     try:
-        res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
+        res = sorted((q.get(timeout=360) for _ in range(world)), key=lambda r: r[0])
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -122,13 +130,16 @@ def test_rowsplit_world2_oneshot_on_gpu(layout):
         assert r[1] != "error", f"rank {r[0]}: {r[2]}"
     for p in procs:
         assert p.exitcode == 0
-    for rank, n_groups, prefill_rel, decode_rel, same, n_tok, failed, sharded, rows, r0, fused_ok in res:
-        assert sharded and rows == 256 and n_groups == 4, (rank, rows, n_groups)
+    rows_exp = 512 // world
+    for rank, n_groups, prefill_rel, decode_rel, same, same_ref, n_tok, failed, sharded, rows, r0, fused_ok in res:
+        assert sharded and rows == rows_exp and n_groups == 4, (rank, rows, n_groups)
         assert fused_ok, "the fused layer was not installed on the shards"
-        assert r0 == 256 * rank                      # q_proj rows [256 rank, +256) of 512
+        assert r0 == rows_exp * rank                 # q_proj rows [rows rank, +rows) of 512
+        if layout.startswith("gather"):
+            assert same_ref, f"rank {rank}: greedy tokens differ from the unsharded model's"
         assert not failed, f"rank {rank}: an exchange timed out"
         # row shards multiply the global state's exact weights; fp32 summation order and the
         # fp16 rounding of a shard launch's outputs are the only differences
         assert prefill_rel < 2e-3 and decode_rel < 2e-3, (rank, prefill_rel, decode_rel)
-        assert same, "the two ranks decoded different tokens"
+        assert same, "the ranks decoded different tokens"
         assert n_tok > 0

@@ -28,8 +28,8 @@ def _tools_ok():
 
 
 def kernel_resources(lib=LIB):
-    """{demangled kernel name: (vgpr_count, agpr_count, private_segment_fixed_size)} for every
-    gfx950 kernel in the library's offload bundles."""
+    """{demangled kernel name: (vgpr_count, agpr_count, private_segment_fixed_size, sgpr_spill_count,
+    vgpr_spill_count)} for every gfx950 kernel in the library's offload bundles."""
     out = {}
     with tempfile.TemporaryDirectory() as d:
         fat = os.path.join(d, "fat.bin")
@@ -55,8 +55,10 @@ def kernel_resources(lib=LIB):
                 name = re.search(r"\.name:\s+(\S+)", ent).group(1)
                 vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", ent).group(1))
                 priv = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", ent).group(1))
+                ssp = re.search(r"\.sgpr_spill_count:\s+(\d+)", ent)
+                vsp = re.search(r"\.vgpr_spill_count:\s+(\d+)", ent)
                 names.append(name)
-                out[name] = (vgpr, agpr, priv)
+                out[name] = (vgpr, agpr, priv, int(ssp.group(1)) if ssp else 0, int(vsp.group(1)) if vsp else 0)
         dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True,
                              check=True).stdout.split("\n")
     return {dm: out[n] for n, dm in zip(names, dem)}
@@ -71,22 +73,19 @@ def _targs(demangled):
 def test_decode_gemv_kernels_fit_without_spills():
     res = kernel_resources()
     checked, bad = 0, []
-    for name, (vgpr, agpr, priv) in res.items():
+    for name, (vgpr, agpr, priv, ssp, vsp) in res.items():
         base = name.split("<")[0].replace("void ", "").strip()
         a = _targs(name)
-        if base == "qz::k_gemv_4bit" and len(a) >= 5:
-            dt, r = int(a[2]), int(a[3])
-        elif base == "qz::k_gemv_4bit_grouped" and len(a) >= 5:
-            dt, r = int(a[2]), int(a[3])
-        elif base == "qz::k_gemv_4bit_pair" and len(a) >= 4:
-            dt, r = int(a[2]), int(a[3])
-        else:
+        # every decode kernel's template starts <DQ, DT, R, ...>
+        if base not in ("qz::k_gemv_4bit", "qz::k_gemv_4bit_grouped", "qz::k_gemv_4bit_pair", "qz::k_mlp_chain") \
+                or len(a) < 4:
             continue
+        dt, r = int(a[1]), int(a[2])
         if dt not in (0, 1) or r > 4:   # 16-bit activations (F16 = 0, BF16 = 1), up to 4 rows per wave
             continue
         checked += 1
-        if agpr > 0 or priv > 0 or vgpr > 256:
-            bad.append((vgpr, agpr, priv, name))
+        if agpr > 0 or priv > 0 or vgpr > 256 or ssp or vsp:
+            bad.append((vgpr, agpr, priv, ssp, vsp, name))
     assert checked > 50, f"only {checked} decode GEMV kernels found in the code objects"
     assert not bad, "decode GEMV kernels that spill:\n" + "\n".join(map(str, sorted(bad, reverse=True)[:20]))
 
@@ -97,13 +96,13 @@ def test_product_decode_picks_keep_two_waves_per_simd():
     stay within 256 VGPRs: at least two waves per SIMD."""
     res = kernel_resources()
     picks = [
-        "qz::k_gemv_4bit_pair<3, true, 0, 4, true, true, true, 8, true, true>",          # gate/up + SiLU + norm
-        "qz::k_gemv_4bit<3, true, 0, 2, 1, 8, false, 0, true, true, true, 0, 0, false, 0>",  # down_proj + residual
-        "qz::k_gemv_4bit_grouped<3, true, 0, 2, 1, true, true, true, 8, false, false>",   # q/k/v + norm
-        "qz::k_gemv_4bit<3, true, 0, 2, 1, 4, false, 0, true, true, false, 0, 8, false, 0>",  # o_proj + residual
+        "qz::k_gemv_4bit_pair<true, 0, 4, true, true, true, true, true>",          # gate/up + SiLU + norm
+        "qz::k_gemv_4bit<true, 0, 2, 1, 8, true, true, true, false, 0>",           # down_proj + residual
+        "qz::k_gemv_4bit_grouped<true, 0, 2, 1, true, true, true, true>",          # q/k/v + norm
+        "qz::k_gemv_4bit<true, 0, 2, 1, 4, true, true, false, true, 0>",           # o_proj + residual
     ]
     for p in picks:
         hits = [v for k, v in res.items() if p in k]
         assert hits, f"{p} not in the library"
-        vgpr, agpr, priv = hits[0]
-        assert vgpr <= 256 and agpr == 0 and priv == 0, (p, vgpr, agpr, priv)
+        vgpr, agpr, priv, ssp, vsp = hits[0]
+        assert vgpr <= 256 and agpr == 0 and priv == 0 and ssp == 0 and vsp == 0, (p, vgpr, agpr, priv, ssp, vsp)

@@ -198,7 +198,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True):
+                         mlp_pair: bool = True, mlp_chain: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -230,7 +230,8 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      mlp=layer_ops in ("all", "all+decoder", "mlp"),
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
-                                     residual=residual, mlp_pair=mlp_pair)  # one launch each
+                                     residual=residual, mlp_pair=mlp_pair,
+                                     mlp_chain=mlp_chain)  # one launch each
     if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -543,7 +544,8 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 
 @torch.inference_mode()
-def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b"):
+def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b",
+                   mlp_chain: bool = True):
     """The Linear4bit chain of a Llama-3 decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
@@ -554,10 +556,13 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     q output in its place, so every launch still depends on the previous one).  Where the product
     takes another form (Llama-3-70B: gate/up at K = 8192 splits rows over two waves, so the pair
     launch refuses and its norm prologue would exceed the workgroup cap), the chain runs what the
-    product runs: norm, grouped gate/up, SiLU product.  shards = P > 1: the same chain on ONE rank's
+    product runs: norm, grouped gate/up, SiLU product.  mlp_chain (one GPU): o_proj + residual, the
+    norm, gate/up + SiLU and down_proj + residual as the ONE persistent launch the product runs
+    (core.gemv_4bit_mlp_chain), so a layer is two launches.  shards = P > 1: the same chain on ONE rank's
     rows of the row-split layout (every projection M / P rows, the launches a rank runs per layer
     at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
-    from quantizations_amd.core import gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
+    from quantizations_amd.core import (gemv_4bit, gemv_4bit_grouped, gemv_4bit_mlp_chain, gemv_4bit_pair_silu,
+                                        mlp_chain_state, quantize_4bit)
     from quantizations_amd.layer_ops import silu_mul
 
     base_cfg = MODELS[model_name]
@@ -592,10 +597,18 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     # consumes the all-gathered [H] / [I] vector; P = 1: the previous output itself)
     full_h = torch.randn(1, 1, I, device=dev).half()
     forms = set()
+    use_chain = mlp_chain and shards == 1
+    cstate = mlp_chain_state(dev) if use_chain else None
 
     def layer(x, w):
         q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
                                         (*w["v"], None, 0, qkv_out[2])], exact_codes=True, norm=(nw1, 1e-5))
+        if use_chain:
+            y = gemv_4bit_mlp_chain(q.view(1, 1, H), x.view(1, 1, H), (*w["o"], None), (*w["gate"], None),
+                                    (*w["up"], None), (*w["down"], None), (nw2, 1e-5), cstate, exact_codes=True)
+            if y is not None:
+                forms.add("o/norm/gate/up/down as ONE persistent launch (qz_mlp_chain)")
+                return y
         xo = q.view(1, 1, H) if shards == 1 else x          # o_proj reads the (gathered) attention output
         a = gemv_4bit(xo, w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1)[:Hs])
         xa = a if shards == 1 else x                        # ... the gathered residual stream
@@ -643,6 +656,7 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
               + gemv_alg_bytes([(Is, H)] * 2) - 2 * H - 2 * Is                  # pair: x once, one output
               + gemv_alg_bytes([(Hs, I)]) + 2 * Hs                              # down_proj + its residual read
               + 2 * (2 * H))                                                    # the two RMSNorm weights
+    failed = bool(cstate[-32].item()) if cstate is not None else False
     del sets, g
     torch.cuda.empty_cache()
     ach = nbytes / (us * 1e-6) / 1e9
@@ -652,6 +666,8 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
                     f"{layers} layers over {copies} rotating weight sets"
                     + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
             "model": model_name, "shards": shards, "gate_up_form": sorted(forms),
+            "launches_per_layer": 2 if any("ONE persistent" in f for f in forms) else 4,
+            "chain_barrier_gave_up": failed,
             "us_per_layer": round(us, 3), "algorithmic_bytes_per_layer": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_layer_min": round(min(times), 3), "us_per_layer_max": round(max(times), 3)}
@@ -1091,6 +1107,8 @@ def main():
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--chain-only", action="store_true",
                     help="only the Linear4bit chain of one decoder layer (chain_roofline; profiling)")
+    ap.add_argument("--chain-three-launch", action="store_true",
+                    help="--chain-only: o_proj / gate-up pair / down_proj as three launches (not the persistent chain)")
     ap.add_argument("--chain-shards", type=int, default=1,
                     help="--chain-only: the chain on one rank's rows of a P-way row split")
     ap.add_argument("--dominant-only", action="store_true",
@@ -1110,6 +1128,9 @@ def main():
                          "stages, the same index)")
     ap.add_argument("--no-mlp-pair", action="store_true",
                     help="gate/up as the grouped launch + a separate SiLU-product launch (default: one launch)")
+    ap.add_argument("--no-mlp-chain", action="store_true",
+                    help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as three launches "
+                         "(default: one persistent launch per layer, csrc/chain.hip)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -1188,7 +1209,8 @@ def main():
         print(json.dumps(dominant_roofline()), flush=True)
         return
     if args.chain_only:
-        print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model)), flush=True)
+        print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model,
+                                        mlp_chain=not args.chain_three_launch)), flush=True)
         return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
@@ -1214,7 +1236,8 @@ def main():
                                                      prenorm=not args.no_prenorm,
                                                      attention=not args.no_attention,
                                                      residual=not args.no_residual,
-                                                     mlp_pair=not args.no_mlp_pair)
+                                                     mlp_pair=not args.no_mlp_pair,
+                                                     mlp_chain=not args.no_mlp_chain)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1270,7 +1293,11 @@ def main():
     if rank == 0 and not args.no_roofline:
         roof = _safe(roofline_object, args, layer_ops)
         parity = _safe(gemv_parity)
-        chain = _safe(chain_roofline)
+        chain = _safe(chain_roofline, mlp_chain=not args.no_mlp_chain)
+        if not args.no_mlp_chain:   # the same chain with the three launches the persistent one replaces
+            c3 = _safe(chain_roofline, mlp_chain=False)
+            if isinstance(chain, dict) and isinstance(c3, dict):
+                chain["three_launch_us_per_layer"] = c3.get("us_per_layer", c3.get("error"))
 
     layer = None
     if not args.no_roofline:
@@ -1323,6 +1350,9 @@ def main():
                                                         and layer_ops in ("all", "all+decoder", "mlp"))
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
+        line["config"]["mlp_chain_launch"] = bool(not args.no_mlp_chain and not args.no_residual and not args.no_attention
+                                                  and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
+                                                  and not sharded)
         line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"
         line["config"]["knobs"] = _safe(effective_knobs)
         if exchange is not None:

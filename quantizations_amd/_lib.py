@@ -90,6 +90,9 @@ SIGNATURES = {
     "qz_allgather_oneshot": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _p],
     "qz_allgather_oneshot_mode": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _i, _p],
     "qz_gemv_knobs": [_p, _i],
+    "qz_gemv_set_knob": [ctypes.c_char_p, _i],
+    "qz_mlp_chain": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _p, _p, _p],
+    "qz_mlp_chain_state_words": [],
     "qz_version": [],
 }
 RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll}
@@ -146,3 +149,9 @@ def gemv_knobs() -> dict:
     buf = ctypes.create_string_buffer(512)
     n = lib.qz_gemv_knobs(buf, len(buf))
     return json.loads(buf.value.decode()) if 0 < n < len(buf) else {}
+
+
+def set_gemv_knob(name: str, value: int) -> None:
+    """Set one decode-launcher knob explicitly (qz_gemv_set_knob); the environment is read only once,
+    at library load."""
+    check(lib.qz_gemv_set_knob(name.encode(), int(value)), f"qz_gemv_set_knob({name})")

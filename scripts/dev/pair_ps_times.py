@@ -12,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from test_gpu_prenorm import _items, DEV  # noqa: E402
+from quantizations_amd import _lib  # noqa: E402
 from quantizations_amd.core import gemv_4bit_pair_silu  # noqa: E402
 
 
@@ -48,9 +49,9 @@ variants = [int(v) for v in os.environ.get("PAIR_PS", "0,2,3,4").split(",")]
 for nrm in ((w, 1e-5), None) if os.environ.get("PAIR_NONORM", "1") == "1" else ((w, 1e-5),):
     ref = None
     for ps in variants:
-        os.environ["QZ_PAIR_PS"] = str(ps % 1000)
+        _lib.set_gemv_knob("QZ_PAIR_PS", ps % 1000)
         # 1000 + v: the 256-B-entry (WT) exact-code table at QZ_PAIR_PS = v; below 1000 the 16-copy one
-        os.environ["QZ_PAIR_WT"] = "1" if ps >= 1000 else "0"
+        _lib.set_gemv_knob("QZ_PAIR_WT", 1 if ps >= 1000 else 0)
         out = [gemv_4bit_pair_silu(x, copies[c], exact_codes=True, norm=nrm) for c in range(NC)]
         if ref is None:
             ref = out
@@ -60,5 +61,5 @@ for nrm in ((w, 1e-5), None) if os.environ.get("PAIR_NONORM", "1") == "1" else (
               f"bit-identical to PS=0: {same}", flush=True)
         if not same:
             sys.exit(3)
-os.environ["QZ_PAIR_PS"] = "0"
-os.environ.pop("QZ_PAIR_WT", None)
+_lib.set_gemv_knob("QZ_PAIR_PS", -1)
+_lib.set_gemv_knob("QZ_PAIR_WT", 1)

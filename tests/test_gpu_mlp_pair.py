@@ -15,6 +15,16 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
+@pytest.fixture
+def knobs():
+    """qz_gemv_set_knob (the library reads its environment once, at load); the defaults come back after."""
+    from quantizations_amd import _lib
+
+    yield _lib.set_gemv_knob
+    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0)):
+        _lib.set_gemv_knob(name, v)
+
+
 def _items(M, K, dtype, seed, quant="nf4", dq=True, bias=False):
     from quantizations_amd.core import quantize_4bit
 
@@ -52,7 +62,7 @@ def test_pair_silu_bit_identical_to_grouped_plus_product(dtype, exact, M, K, nor
 @pytest.mark.filterwarnings("ignore")
 @pytest.mark.parametrize("M,norm,bias,dtype", [(14336, True, False, torch.float16), (14336, False, True, torch.float16),
                                                (3002, True, True, torch.float16), (7168, True, False, torch.bfloat16)])
-def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm, bias, dtype):
+def test_pair_silu_persistent_workgroups_bit_identical(knobs, ps, M, norm, bias, dtype):
     """QZ_PAIR_PS: persistent pair workgroups (ps per CU, or a grid of ps; each taking blocks b, b + grid, ...) give
     the one-workgroup-per-block launch's bits, ragged last block included (K = 4096: two-step waves)."""
     from quantizations_amd.core import gemv_4bit_pair_silu
@@ -62,22 +72,22 @@ def test_pair_silu_persistent_workgroups_bit_identical(monkeypatch, ps, M, norm,
     g = torch.Generator(device="cuda").manual_seed(5)
     x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).to(dtype)
     nrm = ((1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(dtype), 1e-5) if norm else None
-    monkeypatch.setenv("QZ_PAIR_PS", "0")
+    knobs("QZ_PAIR_PS", 0)
     ref = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
-    monkeypatch.setenv("QZ_PAIR_PS", str(ps))
-    for wt in ("0", "1"):   # the 16-copy and the 256-B-entry exact-code tables
-        monkeypatch.setenv("QZ_PAIR_WT", wt)
+    knobs("QZ_PAIR_PS", ps)
+    for wt in (0, 1):   # the 16-copy and the 256-B-entry exact-code tables
+        knobs("QZ_PAIR_WT", wt)
         h = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
         torch.cuda.synchronize()
         assert ref is not None and h is not None
         assert torch.equal(h, ref), wt
-    monkeypatch.delenv("QZ_PAIR_PS")
-    monkeypatch.delenv("QZ_PAIR_WT")   # the product default
+    knobs("QZ_PAIR_PS", -1)
+    knobs("QZ_PAIR_WT", 1)   # the product default
     h = gemv_4bit_pair_silu(x, items, exact_codes=True if dtype == torch.float16 else None, norm=nrm)
     assert torch.equal(h, ref)
 
 
-def test_pair_silu_persistent_fp4_without_double_quant(monkeypatch):
+def test_pair_silu_persistent_fp4_without_double_quant(knobs):
     """The persistent pair (the default with the fused norm) on the FP4 codebook without double quant."""
     from quantizations_amd.core import gemv_4bit_pair_silu
 
@@ -85,9 +95,9 @@ def test_pair_silu_persistent_fp4_without_double_quant(monkeypatch):
     g = torch.Generator(device="cuda").manual_seed(6)
     x = torch.randn(1, 1, 4096, device=DEV, generator=g).half()
     nrm = ((1.0 + 0.1 * torch.randn(4096, device=DEV, generator=g)).half(), 1e-5)
-    monkeypatch.setenv("QZ_PAIR_PS", "0")
+    knobs("QZ_PAIR_PS", 0)
     ref = gemv_4bit_pair_silu(x, items, norm=nrm)
-    monkeypatch.delenv("QZ_PAIR_PS")
+    knobs("QZ_PAIR_PS", -1)
     assert torch.equal(gemv_4bit_pair_silu(x, items, norm=nrm), ref)
 
 

@@ -177,27 +177,3 @@ def _check_prenorm_model(model, cfg, fuse_prenorm, unfuse_prenorm):
         unfuse_prenorm(model)
         toks2, logits2 = greedy(6)
         assert torch.equal(toks2, ref_toks) and torch.equal(logits2[-1], ref_logits[-1])
-
-
-@pytest.mark.parametrize("ps,r,wt", [(2, 2, 0), (3, 1, 0), (2, 1, 1), (2, 2, 1), (512, 4, 0)])
-@pytest.mark.parametrize("Ms,dtype", [((4096, 1024, 1024), torch.float16), ((3000, 8, 1000), torch.float16),
-                                      ((4096, 1024, 1024), torch.bfloat16)])
-def test_grouped_rmsnorm_persistent_workgroups_bit_identical(monkeypatch, ps, r, wt, Ms, dtype):
-    """QZ_GROUPED_PS: persistent workgroups over the blocks of every segment (a workgroup crossing
-    into the next segment re-stages its code2 table) give the default launch's bits."""
-    from quantizations_amd.core import gemv_4bit_grouped
-
-    K = 4096
-    items = _items(Ms, K, dtype, seed=ps + r + len(Ms), bias_seg=1)
-    g = torch.Generator(device="cuda").manual_seed(9)
-    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 3).to(dtype)
-    w = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(dtype)
-    exact = True if dtype == torch.float16 else None
-    ref = gemv_4bit_grouped(x, items, exact_codes=exact, norm=(w, 1e-5))
-    monkeypatch.setenv("QZ_GROUPED_PS", str(ps))
-    monkeypatch.setenv("QZ_GROUPED_PS_R", str(r))
-    monkeypatch.setenv("QZ_GROUPED_WT", str(wt))
-    out = gemv_4bit_grouped(x, items, exact_codes=exact, norm=(w, 1e-5))
-    torch.cuda.synchronize()
-    for a, b in zip(out, ref):
-        assert torch.equal(a, b)

@@ -48,6 +48,7 @@ constexpr int kChWords = kChStatus + kChLine;
 constexpr int kChNW = 8;                            // waves per workgroup (one workgroup per CU)
 constexpr unsigned kChSpinLimit = 1u << 18;         // polls (each >= one sc1 round trip + s_sleep)
 constexpr int kChMaxK = 8192;                       // the normed stage's K (norm image + chunk registers)
+constexpr int kChMaxI = 28672;                      // down_proj's K (its LDS image of act)
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned *p) {
   return __hip_atomic_load((const gu32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -177,7 +178,34 @@ __device__ __forceinline__ unsigned chain_poll(const unsigned *st, int b, int la
   return __builtin_amdgcn_readfirstlane(v);
 }
 
-template <bool DQ, int DT, bool CL, int R>
+// Diagnostic stage stamps (measurement-only builds: diag_stamps.hip defines QZ_STAMPS and
+// instantiates STAMP = 1; the product library compiles none of this): wave 0 of every workgroup
+// records s_memrealtime (100 MHz, chip-wide) at fixed points, stored at the end by lane 0.
+#ifdef QZ_STAMPS
+__device__ unsigned long long *g_qz_chain_stamp;
+#define CH_STAMP(k)                                                                              \
+  do {                                                                                           \
+    if constexpr (STAMP != 0) {                                                                  \
+      if (wave == 0) {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch_st_[k])::"memory");   \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+      }                                                                                          \
+    }                                                                                            \
+  } while (0)
+#define CH_STAMP_FLUSH()                                                                         \
+  do {                                                                                           \
+    if constexpr (STAMP != 0) {                                                                  \
+      if (threadIdx.x == 0)                                                                      \
+        for (int k_ = 0; k_ < 12; ++k_) g_qz_chain_stamp[(size_t)blockIdx.x * 12 + k_] = ch_st_[k_]; \
+    }                                                                                            \
+  } while (0)
+#else
+#define CH_STAMP(k) do {} while (0)
+#define CH_STAMP_FLUSH() do {} while (0)
+#endif
+
+template <bool DQ, int DT, bool CL, int R, int STAMP = 0>
 __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
   static_assert(DT == QZ_DT_F16 || DT == QZ_DT_BF16, "16-bit activations");
   static_assert(!CL || DT == QZ_DT_F16, "exact codes are the fp16-activation table");
@@ -194,6 +222,10 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+#ifdef QZ_STAMPS
+  unsigned long long ch_st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  CH_STAMP(0);
   const int P = (int)gridDim.x;
   const int W = P * NW;
   const int gw = (int)blockIdx.x * NW + wave;
@@ -331,6 +363,7 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
     }
   }
 
+  CH_STAMP(1);   // stage A done
   // ============ barrier 0 (h1 published) + stage B's first block ============
   const bool is_up = wave >= 4;
   const int rg = wave & 3;
@@ -352,6 +385,7 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its h1 stores have completed
   __syncthreads();
+  CH_STAMP(2);   // every wave drained its h1 stores
   if (threadIdx.x == 0) chain_arrive(st, 0);
   unsigned seen = chain_poll(st, 0, lane);
   b_cur.issue_w(pb, (min(blk, nblocksB - 1) * 4 + rg) * R, 0, lane);
@@ -365,6 +399,7 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
   }
   __syncthreads();
 
+  CH_STAMP(3);   // barrier 0 passed
   // ============ stage B: x' = RMSNorm(h1) into LDS (k_rmsnorm's order), then the gate/up pair ============
   {
     // threads 0..255 (k_rmsnorm's 256-thread order): chunks t, t + 256, ... squared in element order;
@@ -397,6 +432,7 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
     }
     __syncthreads();
   }
+  CH_STAMP(4);   // x' in LDS
   {
     const float offB = DQ ? *keep_sp((is_up ? c.up : c.gate).sc.offset) : 0.0f;
     const int tbl = is_up ? 2 : 1;
@@ -449,11 +485,12 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
     }
   }
 
+  CH_STAMP(5);   // stage B done
   // ============ barrier 1 (act published) + stage C's first unit ============
   const StageParams pd = load_stage<DQ>(c.down);
   const int nsC = pd.K >> 11;
   const int unitsC = pd.M / R;
-  typedef ChainLoads<DQ, R, 2> LoadsC;
+  typedef ChainLoads<DQ, R, 1> LoadsC;   // x = the workgroup's LDS image of act
   LoadsC c_cur, c_oth;
   u = gw;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its act stores have completed
@@ -471,10 +508,22 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
   }
   __syncthreads();
 
+  CH_STAMP(6);   // barrier 1 passed
   // ============ stage C: out = h1 + down_proj(act) ============
   {
-    c_cur.issue_x(pd);
-    c_oth.issue_x(pd);
+    // act (handed off) into the workgroup's LDS image once, with sc1 loads, in the norm image's
+    // conflict-free layout (every wave then reads its x slices from LDS, as stage B does: sc1 loads
+    // bypass L1, and every wave reading its slices of act from the fabric moved 8x the bytes)
+    const int nchunkC = pd.K >> 3;
+    const void *actp = keep_sp(c.down.x);
+#pragma unroll
+    for (int i = 0; i < kChMaxI / 8 / (NW * 64); ++i) {
+      const int ch = (int)threadIdx.x + i * NW * 64;
+      if (ch < nchunkC)
+        *reinterpret_cast<u32x4 *>(s_x + norm_x_off((uint32_t)ch)) = ld16_sc1(actp, (uint32_t)ch * 16u);
+    }
+    __syncthreads();
+    CH_STAMP(7);   // act in LDS
     const float offC = DQ ? *keep_sp(c.down.sc.offset) : 0.0f;
     for (;;) {
       run_steps(c_cur, c_oth, pd, min(u, unitsC - 1) * R, nsC, 3, offC);
@@ -517,8 +566,11 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
     }
   }
 
+  CH_STAMP(8);   // stage C done (wave 0)
   // ============ finish: the last workgroup advances the epoch ============
   __syncthreads();
+  CH_STAMP(9);   // every wave done
+  CH_STAMP_FLUSH();
   if (threadIdx.x == 0) {
     if (!ok) __hip_atomic_store((gu32_t *)(st + kChStatus), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned t = __hip_atomic_fetch_add((gu32_t *)(st + kChDone), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -531,10 +583,10 @@ __global__ __launch_bounds__(kChNW * 64, 1) void k_mlp_chain(ChainArgs c) {
 
 // the grid: one workgroup per CU (the dynamic LDS request keeps a second one off every CU), all
 // resident -- the grid barriers need every workgroup running; 0 if the device cannot hold it
-template <bool DQ, int DT, bool CL, int R>
+template <bool DQ, int DT, bool CL, int R, int STAMP = 0>
 static int chain_grid(size_t lds) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(&k_mlp_chain<DQ, DT, CL, R>),
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(&k_mlp_chain<DQ, DT, CL, R, STAMP>),
                                                    kChNW * 64, lds) != hipSuccess || occ < 1)
     return 0;
   return device_cus();
@@ -546,10 +598,11 @@ using namespace qz;
 
 extern "C" int qz_mlp_chain_state_words(void) { return kChWords; }
 
-extern "C" int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz_gemv_segment *up,
-                            const qz_gemv_segment *down, const void *x, const void *residual, int dtype,
-                            int quant_type, int blocksize, int blocksize2, const void *norm_weight, float eps,
-                            void *h1, void *act, void *out, unsigned *state, void *stream) {
+// Validates the chain's arguments and fills its kernel arguments; *H_, *I_ the widths.  QZ_OK or a status.
+static int chain_args(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz_gemv_segment *up,
+                      const qz_gemv_segment *down, const void *x, const void *residual, int dtype, int quant_type,
+                      int blocksize, int blocksize2, const void *norm_weight, float eps, void *h1, void *act, void *out,
+                      unsigned *state, ChainArgs *c, bool *cl_, bool *dq_, size_t *lds_) {
   if (!o || !gate || !up || !down || !x || !residual || !norm_weight || !h1 || !act || !out || !state)
     return QZ_ERR_ARG;
   if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_SHAPE;
@@ -557,9 +610,8 @@ extern "C" int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gat
   if (up->M != I || down->M != H || H <= 0 || I <= 0) return QZ_ERR_SHAPE;
   const bool cl = exact_codes(quant_type, nullptr) && dtype == QZ_DT_F16;
   const bool dq = o->qabsmax != nullptr;
-  ChainArgs c;
   const qz_gemv_segment *segs[4] = {o, gate, up, down};
-  GemvParams *ps[4] = {&c.o, &c.gate, &c.up, &c.down};
+  GemvParams *ps[4] = {&c->o, &c->gate, &c->up, &c->down};
   const int Ks[4] = {H, H, H, I};
   const void *xs[4] = {x, nullptr, nullptr, act};
   void *ys[4] = {h1, act, act, out};
@@ -578,23 +630,32 @@ extern "C" int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gat
     ps[i]->x = xs[i];
     ps[i]->res = rs[i];
   }
-  // shapes: whole R-row units everywhere (R = 2), 16-B act pieces per pair block, the normed K
+  // shapes: whole R-row units everywhere (R = 2), 16-B act pieces per pair block, the LDS images
   constexpr int R = 2;
-  if (H % (4 * R) || I % (4 * R) || H > kChMaxK || H % 2048 || I % 2048 ||
+  if (H % (4 * R) || I % (4 * R) || H > kChMaxK || I > kChMaxI || H % 2048 || I % 2048 ||
       ((uintptr_t)x | (uintptr_t)residual | (uintptr_t)norm_weight | (uintptr_t)h1 | (uintptr_t)act | (uintptr_t)out) % 16)
     return QZ_ERR_SHAPE;
-  c.nw = norm_weight;
-  c.eps = eps;
-  c.state = state;
-  hipStream_t s = (hipStream_t)stream;
-  // dynamic LDS: the x' image (H * 2 B), at least 24 KiB so that the workgroup's whole request
-  // (64 KiB table + 4 KiB code tables + this) exceeds half the CU's 160 KiB: one workgroup per CU
-  const size_t lds = max((size_t)H * 2, (size_t)24 << 10);
+  c->nw = norm_weight;
+  c->eps = eps;
+  c->state = state;
+  *cl_ = cl;
+  *dq_ = dq;
+  // dynamic LDS: the x' image of stage B (H * 2 B), then stage C's act image (I * 2 B), at least
+  // 24 KiB so that the workgroup's whole request (64 KiB table + 4 KiB code tables + this) exceeds
+  // half the CU's 160 KiB: one workgroup per CU
+  *lds_ = max(max((size_t)H * 2, (size_t)I * 2), (size_t)24 << 10);
+  return QZ_OK;
+}
+
+template <int STAMP>
+static int chain_launch(const ChainArgs &c, int dtype, bool cl, bool dq, size_t lds, hipStream_t s, int *grid_out) {
+  constexpr int R = 2;
+  int grid = 0;
 #define QZ_CH(DQ_, DT_, CL_)                                                                                 \
   do {                                                                                                     \
-    const int grid = chain_grid<DQ_, DT_, CL_, R>(lds);                                                    \
+    grid = chain_grid<DQ_, DT_, CL_, R, STAMP>(lds);                                                       \
     if (grid < 8) return QZ_ERR_SHAPE;                                                                     \
-    hipLaunchKernelGGL((k_mlp_chain<DQ_, DT_, CL_, R>), dim3(grid), dim3(kChNW * 64), lds, s, c);          \
+    hipLaunchKernelGGL((k_mlp_chain<DQ_, DT_, CL_, R, STAMP>), dim3(grid), dim3(kChNW * 64), lds, s, c);   \
   } while (0)
   if (dtype == QZ_DT_F16) {
     if (dq) { if (cl) QZ_CH(true, QZ_DT_F16, true); else QZ_CH(true, QZ_DT_F16, false); }
@@ -604,5 +665,19 @@ extern "C" int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gat
   }
 #undef QZ_CH
   QZ_LAUNCH_CHECK();
+  if (grid_out) *grid_out = grid;
   return QZ_OK;
+}
+
+extern "C" int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz_gemv_segment *up,
+                            const qz_gemv_segment *down, const void *x, const void *residual, int dtype,
+                            int quant_type, int blocksize, int blocksize2, const void *norm_weight, float eps,
+                            void *h1, void *act, void *out, unsigned *state, void *stream) {
+  ChainArgs c;
+  bool cl, dq;
+  size_t lds;
+  const int rc = chain_args(o, gate, up, down, x, residual, dtype, quant_type, blocksize, blocksize2, norm_weight, eps,
+                            h1, act, out, state, &c, &cl, &dq, &lds);
+  if (rc != QZ_OK) return rc;
+  return chain_launch<0>(c, dtype, cl, dq, lds, (hipStream_t)stream, nullptr);
 }

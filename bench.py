@@ -198,7 +198,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = True):
+                         mlp_pair: bool = True, mlp_chain: bool = False):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -545,7 +545,7 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 @torch.inference_mode()
 def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b",
-                   mlp_chain: bool = True):
+                   mlp_chain: bool = False):
     """The Linear4bit chain of a Llama-3 decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
@@ -1107,8 +1107,9 @@ def main():
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--chain-only", action="store_true",
                     help="only the Linear4bit chain of one decoder layer (chain_roofline; profiling)")
-    ap.add_argument("--chain-three-launch", action="store_true",
-                    help="--chain-only: o_proj / gate-up pair / down_proj as three launches (not the persistent chain)")
+    ap.add_argument("--chain-persistent", action="store_true",
+                    help="--chain-only: o_proj .. down_proj as the ONE persistent launch (csrc/chain.hip) instead of the "
+                         "product's three launches")
     ap.add_argument("--chain-shards", type=int, default=1,
                     help="--chain-only: the chain on one rank's rows of a P-way row split")
     ap.add_argument("--dominant-only", action="store_true",
@@ -1128,9 +1129,10 @@ def main():
                          "stages, the same index)")
     ap.add_argument("--no-mlp-pair", action="store_true",
                     help="gate/up as the grouped launch + a separate SiLU-product launch (default: one launch)")
-    ap.add_argument("--no-mlp-chain", action="store_true",
-                    help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as three launches "
-                         "(default: one persistent launch per layer, csrc/chain.hip)")
+    ap.add_argument("--mlp-chain", action="store_true",
+                    help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
+                         "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
+                         "barriers cost more than launch boundaries, DESIGN.md section 12)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -1210,7 +1212,7 @@ def main():
         return
     if args.chain_only:
         print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model,
-                                        mlp_chain=not args.chain_three_launch)), flush=True)
+                                        mlp_chain=args.chain_persistent)), flush=True)
         return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
@@ -1237,7 +1239,7 @@ def main():
                                                      attention=not args.no_attention,
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
-                                                     mlp_chain=not args.no_mlp_chain)
+                                                     mlp_chain=args.mlp_chain)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1293,11 +1295,7 @@ def main():
     if rank == 0 and not args.no_roofline:
         roof = _safe(roofline_object, args, layer_ops)
         parity = _safe(gemv_parity)
-        chain = _safe(chain_roofline, mlp_chain=not args.no_mlp_chain)
-        if not args.no_mlp_chain:   # the same chain with the three launches the persistent one replaces
-            c3 = _safe(chain_roofline, mlp_chain=False)
-            if isinstance(chain, dict) and isinstance(c3, dict):
-                chain["three_launch_us_per_layer"] = c3.get("us_per_layer", c3.get("error"))
+        chain = _safe(chain_roofline, mlp_chain=args.mlp_chain)
 
     layer = None
     if not args.no_roofline:
@@ -1350,7 +1348,7 @@ def main():
                                                         and layer_ops in ("all", "all+decoder", "mlp"))
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
-        line["config"]["mlp_chain_launch"] = bool(not args.no_mlp_chain and not args.no_residual and not args.no_attention
+        line["config"]["mlp_chain_launch"] = bool(args.mlp_chain and not args.no_residual and not args.no_attention
                                                   and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
                                                   and not sharded)
         line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"

@@ -417,7 +417,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
                    decoder: bool = False, attention: bool = True, residual: bool = True,
-                   mlp_pair: bool = True, mlp_chain: bool = True) -> int:
+                   mlp_pair: bool = True, mlp_chain: bool = False) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -432,10 +432,11 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     once per module).  `residual` (with `attention` and `mlp`) moves each decoder layer's two
     residual adds into the o_proj / down_proj GEMV epilogues (counted once per layer).
     `mlp_pair` lets a fused MLP compute gate/up and act_fn(gate) * up in one launch
-    (modules.linear4bit_silu_pair) where its projections form a decode group.  `mlp_chain` (with
-    `residual`) lets a residual-fused decoder layer run a decode token's o_proj + residual,
+    (modules.linear4bit_silu_pair) where its projections form a decode group.  `mlp_chain` (opt-in,
+    with `residual`) lets a residual-fused decoder layer run a decode token's o_proj + residual,
     post-attention norm, MLP and second residual as ONE persistent launch (_mlp_chain) where the
-    layer qualifies (after fuse_prenorm)."""
+    layer qualifies (after fuse_prenorm): bit-identical, but measured slower than the three launches
+    (each in-kernel grid barrier costs 6-7 us against a ~1.5 us launch boundary)."""
     import sys
 
     n = 0

@@ -150,7 +150,7 @@ def test_llama_decode_with_the_chain_equals_three_launches(dtype):
     import quantizations_amd.integration as integ
 
     cfg, model = _model(dtype)
-    bench.prepare_decode_model(model, 0, 1, False)
+    bench.prepare_decode_model(model, 0, 1, False, mlp_chain=True)
     calls = {"n": 0}
     orig = integ._mlp_chain
 
@@ -178,7 +178,7 @@ def test_llama_single_token_logits_identical():
     import bench
 
     cfg, model = _model(torch.float16, layers=3)
-    bench.prepare_decode_model(model, 0, 1, False)
+    bench.prepare_decode_model(model, 0, 1, False, mlp_chain=True)
     ids = torch.randint(0, cfg.vocab_size, (1, 10), generator=torch.Generator().manual_seed(3)).to(DEV)
     from transformers.cache_utils import StaticCache
 

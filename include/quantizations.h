@@ -355,7 +355,7 @@ int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz
 int qz_mlp_chain_state_words(void);
 
 /* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
- * QZ_PAIR_WT, QZ_PAIR_PS: environment variables read ONCE when the library is loaded) and the
+ * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1: environment variables read ONCE when the library is loaded) and the
  * device's CU count, as a JSON object written to buf (NUL-terminated when n > the length).
  * Returns the length of the JSON text.  No reference counterpart (measurement bookkeeping). */
 int qz_gemv_knobs(char *buf, int n);

@@ -56,6 +56,7 @@ static Knobs read_knobs() {
   k.pair_r = (pr == 2 || pr == 3 || pr == 4 || pr == 6 || pr == 8) ? pr : 0;
   k.pair_wt = env_int("QZ_PAIR_WT", 1) != 0;
   k.pair_ps = env_int("QZ_PAIR_PS", -1);
+  k.pair_wk1 = env_int("QZ_PAIR_WK1", 1) != 0;
   return k;
 }
 static Knobs g_knobs = read_knobs();   // at library load
@@ -367,9 +368,21 @@ extern "C" int qz_gemv_4bit_grouped_rmsnorm(int nseg, const qz_gemv_segment *seg
 // the persistent exact-code pair on the 256-B-entry table (64 KiB: 32 bank-private copies of each 8-B
 // entry, v_perm addresses), 2 workgroups per CU
 template <bool DQ, int DT, int R, bool CL, bool NRM>
-static void launch_pair_wt(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g) {
-  if constexpr (CL && NRM && DT == QZ_DT_F16 && (R == 2 || R == 4))
-    hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, true, true, true>), dim3(grid), dim3(256), lds, s, g);
+static void launch_pair_wt(unsigned grid, size_t lds, hipStream_t s, const GemvGroup &g, bool two) {
+  if constexpr (CL && NRM && DT == QZ_DT_F16 && (R == 2 || R == 4)) {
+    if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, true, true, true>), dim3(grid), dim3(256), lds, s, g);
+    else hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, false, true, true>), dim3(grid), dim3(256), lds, s, g);
+  }
+}
+
+// the persistent pair in its step-loop form (K != 4096): with the fused norm only -- without one
+// the persistence buys nothing (the knob's grid then runs one workgroup per block)
+template <bool DQ, int DT, int R, bool CL, bool NRM>
+static void launch_pair_ps_loop(unsigned grid, int blocks, size_t lds, hipStream_t s, const GemvGroup &g) {
+  if constexpr (NRM)
+    hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, false, true>), dim3(grid), dim3(256), lds, s, g);
+  else
+    hipLaunchKernelGGL((k_gemv_4bit_pair<DQ, DT, R, CL, NRM, false>), dim3(blocks), dim3(256), lds, s, g);
 }
 
 // LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) (modeling_llama.py:175, hidden_act "silu") in one
@@ -401,12 +414,15 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   if (norm_weight && (K % 8 != 0 || K > 16384 || ((uintptr_t)x | (uintptr_t)norm_weight) % 16 != 0))
     return QZ_ERR_SHAPE;
   // the geometry qz_gemv_4bit_grouped takes for the pair's 2M rows (same per-row summation order,
-  // so the same bits); the epilogue needs whole rows per wave: splits along K (WK > 1, e.g. the
-  // K = 8192 layers) are left to the two-launch form.  Single-row waves (R = 1: small row shards,
-  // e.g. Llama-3-8B gate/up over 8 ranks) take the pair launch too
+  // so the same bits); the epilogue needs whole rows per wave, so where the grouped launch splits K
+  // over two waves (WK = 2: the K = 8192 layers of Llama-3-70B) the pair keeps the rows whole
+  // (WK = 1, same R: a different fp32 summation order from the grouped launch there, the same
+  // products).  Single-row waves (R = 1: small row shards, e.g. Llama-3-8B gate/up over 8 ranks)
+  // take the pair launch too
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
-  if (WK != 1) return QZ_ERR_SHAPE;
+  if (WK != 1 && !gemv_knobs().pair_wk1) return QZ_ERR_SHAPE;
+  WK = 1;
   if (gemv_knobs().pair_r) R = gemv_knobs().pair_r;   // knob; the per-row sums do not depend on R
   const int blocks = (M + 2 * R - 1) / (2 * R);
   if (norm_weight && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
@@ -435,13 +451,14 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
     pgrid_i = (wt_ok ? 2 : 3) * cus;
   }
   const unsigned pgrid = (unsigned)max(pgrid_i, 1);
-  const bool persist = two && pgrid_i > 0 && pgrid_i < blocks;
+  const bool persist = pgrid_i > 0 && pgrid_i < blocks;   // the two-step form or the step loop (K != 4096)
   const bool pair_wt = persist && wt_ok;
 #define QZ_PS(DQ_, DT_, RR, CL_, NRM_)                                                                               \
   do {                                                                                                              \
-    if (pair_wt) launch_pair_wt<DQ_, DT_, RR, CL_, NRM_>(pgrid, lds, s, g);                                        \
-    else if (persist) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, true, true>), dim3(pgrid),      \
-                                         dim3(256), lds, s, g);                                                     \
+    if (pair_wt) launch_pair_wt<DQ_, DT_, RR, CL_, NRM_>(pgrid, lds, s, g, two);                                        \
+    else if (persist && two) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, true, true>), dim3(pgrid), \
+                                                dim3(256), lds, s, g);                                              \
+    else if (persist) launch_pair_ps_loop<DQ_, DT_, RR, CL_, NRM_>(pgrid, blocks, lds, s, g);                      \
     else if (two) hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, true>), dim3(blocks), dim3(256),    \
                                      lds, s, g);                                                                    \
     else hipLaunchKernelGGL((k_gemv_4bit_pair<DQ_, DT_, RR, CL_, NRM_, false>), dim3(blocks), dim3(256), lds, s, g); \
@@ -478,8 +495,9 @@ extern "C" int qz_gemv_knobs(char *buf, int n) {
   char tmp[256];
   const int len = snprintf(tmp, sizeof(tmp),
                            "{\"QZ_GEMV_WIDE8\": %d, \"QZ_GROUPED_NORM_R\": %d, \"QZ_PAIR_R\": %d, \"QZ_PAIR_WT\": %d, "
-                           "\"QZ_PAIR_PS\": %d, \"cus\": %d}",
-                           gemv_knobs().wide8, gemv_knobs().norm_r, gemv_knobs().pair_r, gemv_knobs().pair_wt, gemv_knobs().pair_ps, device_cus());
+                           "\"QZ_PAIR_PS\": %d, \"QZ_PAIR_WK1\": %d, \"cus\": %d}",
+                           gemv_knobs().wide8, gemv_knobs().norm_r, gemv_knobs().pair_r, gemv_knobs().pair_wt,
+                           gemv_knobs().pair_ps, gemv_knobs().pair_wk1, device_cus());
   if (buf && n > len) memcpy(buf, tmp, (size_t)len + 1);
   return len;
 }
@@ -494,6 +512,7 @@ extern "C" int qz_gemv_set_knob(const char *name, int value) {
   else if (!strcmp(name, "QZ_PAIR_R")) k.pair_r = (value == 2 || value == 3 || value == 4 || value == 6 || value == 8) ? value : 0;
   else if (!strcmp(name, "QZ_PAIR_WT")) k.pair_wt = value != 0;
   else if (!strcmp(name, "QZ_PAIR_PS")) k.pair_ps = value;
+  else if (!strcmp(name, "QZ_PAIR_WK1")) k.pair_wk1 = value != 0;
   else return QZ_ERR_ARG;
   return QZ_OK;
 }

@@ -591,7 +591,7 @@ template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, boo
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block, const GemvParams *pair = nullptr) {
   static_assert(!NRM || (NW == 4 && FS && DT != QZ_DT_F32), "fused pre-norm: 4 waves, full steps, 16-bit activations");
   static_assert(!PAIR || (NW == 4 && WK == 1 && DT != QZ_DT_F32), "pair: 4 waves, WK = 1, 16-bit activations");
-  static_assert(!PS || (PAIR && TWO), "persistent form: two-step pair launches");
+  static_assert(!PS || (PAIR && FS), "persistent form: pair launches, full steps");
   static_assert(!TWO || (FS && WK == 1), "two-step form: full steps, whole rows per wave");
   static_assert(!CL || DT == QZ_DT_F16, "exact codes are the fp16-activation table");
   static_assert(NW * 64 >= 256, "one byte-table entry per thread");
@@ -794,10 +794,40 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     const int nblocks = (p.M + 2 * R - 1) / (2 * R);
     int blk = block;
     for (int it = 0;; ++it) {
-      other.issue(p, row0, s + WK, lane, row_bytes);
-      __builtin_amdgcn_sched_barrier(0);
-      consume(cur);
-      consume(other);
+      if constexpr (TWO) {
+        other.issue(p, row0, s + WK, lane, row_bytes);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(cur);
+        consume(other);
+      } else {
+        // n_my steps (WK = 1: every step of the row), cur = step 0 issued: the early ping-pong --
+        // `other` one step ahead, each set re-issued right after it is consumed
+        const int n = n_my;
+        other.issue(p, row0, n >= 2 ? 1 : 0, lane, row_bytes);
+        __builtin_amdgcn_sched_barrier(0);
+        int j = 0, ss = 0;
+        for (; j + 3 < n; j += 2) {
+          consume(cur);
+          cur.issue(p, row0, ss + 2, lane, row_bytes);
+          __builtin_amdgcn_sched_barrier(0);
+          consume(other);
+          other.issue(p, row0, ss + 3, lane, row_bytes);
+          __builtin_amdgcn_sched_barrier(0);
+          ss += 2;
+        }
+        if (n - j == 3) {
+          consume(cur);
+          cur.issue(p, row0, ss + 2, lane, row_bytes);
+          __builtin_amdgcn_sched_barrier(0);
+          consume(other);
+          consume(cur);
+        } else if (n - j == 2) {
+          consume(cur);
+          consume(other);
+        } else {
+          consume(cur);
+        }
+      }
       const int nb = blk + (int)gridDim.x;   // workgroup-uniform
       if (nb >= nblocks) {
         pair_out(blk, it & 1);
@@ -940,6 +970,8 @@ struct Knobs {
   int pair_r;   // QZ_PAIR_R=2|3|4|6|8: rows per wave of the pair launch (0 = geometry's)
   int pair_wt;  // QZ_PAIR_WT=0: the persistent pair keeps the 16-copy exact table (default 1)
   int pair_ps;  // QZ_PAIR_PS: 0 = one workgroup per block, 1..8 = workgroups per CU, >= 16 = the grid; -1 = default
+  int pair_wk1; // QZ_PAIR_WK1=0: where the grouped geometry splits K over two waves (K = 8192), the pair launch
+                // refuses (the round-4 behaviour: grouped launch + separate norm / SiLU launches); default 1
 };
 // the knobs the library read at load (gemv.hip); qz_gemv_set_knob changes one explicitly
 Knobs &gemv_knobs();

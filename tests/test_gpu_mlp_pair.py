@@ -192,3 +192,28 @@ def test_llama_mlp_pair_logits_bit_identical_to_transformers_mlp():
             assert all(torch.equal(a, b) for a, b in zip(got, ref))
     finally:
         unfuse_layer_ops(model)
+
+
+@pytest.mark.parametrize("M,norm", [(28672, True), (3584, True), (28672, False)])
+def test_pair_silu_k8192_against_fp64(M, norm):
+    """K = 8192 (Llama-3-70B gate/up, whole and its 8-way row shard): the pair launch keeps whole rows
+    per wave (the grouped launch splits K over two waves there, so the two differ in fp32 summation
+    order) -- held to the fp64 product of the bit-exact dequantised weights through the norm and SiLU,
+    within fp16 rounding; persistent workgroups and the step loop where the norm rides in it."""
+    from quantizations_amd.core import dequantize_4bit, gemv_4bit_pair_silu
+
+    K = 8192
+    items = _items(M, K, torch.float16, seed=M + 1)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).half()
+    nw = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).half()
+    h = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=(nw, 1e-5) if norm else None)
+    torch.cuda.synchronize()
+    assert h is not None
+    xd = x.double().view(-1)
+    if norm:
+        xd = (nw.double() * (xd * torch.rsqrt((xd * xd).mean() + 1e-5)).half().double()).half().double()
+    gv, uv = [(dequantize_4bit(p, s, out_dtype=torch.float32).t().double() @ xd).half().double() for p, s, _ in items]
+    ref = (gv / (1 + torch.exp(-gv))).half().double() * uv
+    rel = ((h.double().view(-1) - ref).norm() / ref.norm()).item()
+    assert rel < 2e-3, rel

@@ -14,9 +14,11 @@ step() {  # name timeout cmd...
   echo "== $name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-400
   [ $rc -eq 0 ] || exit $rc
 }
-step r5d_tests 400 python -u -m pytest tests/test_gpu_mlp_pair.py tests/test_gpu_prenorm.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread
-step r5d_chain70 300 python bench.py --model llama3-70b --chain-only
-step r5d_chain70_old 300 env QZ_PAIR_WK1=0 python bench.py --model llama3-70b --chain-only
-step r5d_bench70 900 python bench.py --model llama3-70b --no-prefill --no-cpu --no-roofline --steps 32 --warmup 4
-step r5d_bench70_old 900 env QZ_PAIR_WK1=0 python bench.py --model llama3-70b --no-prefill --no-cpu --no-roofline --steps 32 --warmup 4
+[ "${1:-}" = bench ] && rm -f gpurun_out/r5d_tests.log
+[ "${1:-}" = bench ] || step r5d_tests 400 python -u -m pytest tests/test_gpu_mlp_pair.py tests/test_gpu_prenorm.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread
+[ "${1:-}" = bench ] || step r5d_chain70 300 python bench.py --model llama3-70b --chain-only
+[ "${1:-}" = bench ] || step r5d_chain70_old 300 env QZ_PAIR_WK1=0 python bench.py --model llama3-70b --chain-only
+[ "${1:-}" = bench ] || { echo done; exit 0; }
+step r5d_bench70 540 python bench.py --model llama3-70b --no-prefill --no-cpu --no-roofline --steps 32 --warmup 4
+step r5d_bench70_old 540 env QZ_PAIR_WK1=0 python bench.py --model llama3-70b --no-prefill --no-cpu --no-roofline --steps 32 --warmup 4
 echo done

@@ -21,7 +21,7 @@ def knobs():
     from quantizations_amd import _lib
 
     yield _lib.set_gemv_knob
-    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0)):
+    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0), ("QZ_PAIR_WK1", 1)):
         _lib.set_gemv_knob(name, v)
 
 
@@ -135,15 +135,31 @@ def test_pair_silu_on_row_shards(world, rank):
     assert torch.equal(h.reshape(-1), full.reshape(-1)[r0:r1])
 
 
+@pytest.mark.parametrize("M,K", [(4096, 8192), (1000, 6144)])
+def test_pair_silu_keeps_rows_whole_where_grouped_splits_k(knobs, M, K):
+    """Geometries where the grouped launch splits K over two waves (K = 8192; small pairs): the pair
+    keeps whole rows per wave (round 5) -- the same products in another fp32 summation order, so it
+    matches the grouped launch + product within fp16 rounding; with QZ_PAIR_WK1=0 it declines as in
+    round 4 (None, nothing launched: the grouped launch + product then run)."""
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
+
+    items = _items(M, K, torch.float16, seed=M)
+    x = torch.randn(1, 1, K, device=DEV).half()
+    h = gemv_4bit_pair_silu(x, items, exact_codes=True)
+    gate, up = gemv_4bit_grouped(x, items, exact_codes=True)
+    ref = (F.silu(gate.float()) * up.float())
+    assert h is not None
+    rel = ((h.float() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-3, rel
+    knobs("QZ_PAIR_WK1", 0)
+    assert gemv_4bit_pair_silu(x, items, exact_codes=True) is None
+    knobs("QZ_PAIR_WK1", 1)
+
+
 def test_pair_silu_declines_what_it_cannot_take():
-    """Geometries that split rows over waves (K = 8192; small pairs), odd K, fp32 x, unequal
-    shapes: None, nothing launched (the grouped launch + product then run)."""
+    """Odd K, fp32 x, unequal shapes: None, nothing launched (the grouped launch + product then run)."""
     from quantizations_amd.core import gemv_4bit_pair_silu
 
-    items = _items(4096, 8192, torch.float16, seed=1)
-    assert gemv_4bit_pair_silu(torch.randn(1, 1, 8192, device=DEV).half(), items) is None
-    items = _items(1000, 6144, torch.float16, seed=7)
-    assert gemv_4bit_pair_silu(torch.randn(1, 1, 6144, device=DEV).half(), items) is None
     items = _items(512, 1000, torch.float16, seed=2)
     assert gemv_4bit_pair_silu(torch.randn(1, 1, 1000, device=DEV).half(), items) is None
     items = _items(512, 2048, torch.float32, seed=3)

@@ -554,15 +554,15 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     single-launch roofline with the dependent-launch gaps of a real decode step included (the
     attention launch between q/k/v and o_proj is left out: it is not a Linear4bit; o_proj reads the
     q output in its place, so every launch still depends on the previous one).  Where the product
-    takes another form (Llama-3-70B: gate/up at K = 8192 splits rows over two waves, so the pair
-    launch refuses and its norm prologue would exceed the workgroup cap), the chain runs what the
-    product runs: norm, grouped gate/up, SiLU product.  mlp_chain (one GPU): o_proj + residual, the
+    takes another form (Llama-3-70B: gate/up at K = 8192 splits rows over two waves, so the split
+    pair runs after a separate norm launch), the chain runs what the product runs; `gate_up_form` and
+    `launches_per_layer` say which.  mlp_chain (one GPU): o_proj + residual, the
     norm, gate/up + SiLU and down_proj + residual as the ONE persistent launch the product runs
     (core.gemv_4bit_mlp_chain), so a layer is two launches.  shards = P > 1: the same chain on ONE rank's
     rows of the row-split layout (every projection M / P rows, the launches a rank runs per layer
     at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
-    from quantizations_amd.core import (gemv_4bit, gemv_4bit_grouped, gemv_4bit_mlp_chain, gemv_4bit_pair_silu,
-                                        mlp_chain_state, quantize_4bit)
+    from quantizations_amd.core import (LAST_FORM, gemv_4bit, gemv_4bit_grouped, gemv_4bit_mlp_chain,
+                                        gemv_4bit_pair_silu, mlp_chain_state, quantize_4bit)
     from quantizations_amd.layer_ops import silu_mul
 
     base_cfg = MODELS[model_name]
@@ -597,17 +597,21 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     # consumes the all-gathered [H] / [I] vector; P = 1: the previous output itself)
     full_h = torch.randn(1, 1, I, device=dev).half()
     forms = set()
+    launches = []   # per layer, as the forms ran (a norm launch counts)
     use_chain = mlp_chain and shards == 1
     cstate = mlp_chain_state(dev) if use_chain else None
 
     def layer(x, w):
         q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
                                         (*w["v"], None, 0, qkv_out[2])], exact_codes=True, norm=(nw1, 1e-5))
+        n = 2 if LAST_FORM.get("grouped", "").startswith("norm launch") else 1
+        forms.add("q/k/v " + LAST_FORM.get("grouped", "?"))
         if use_chain:
             y = gemv_4bit_mlp_chain(q.view(1, 1, H), x.view(1, 1, H), (*w["o"], None), (*w["gate"], None),
                                     (*w["up"], None), (*w["down"], None), (nw2, 1e-5), cstate, exact_codes=True)
             if y is not None:
                 forms.add("o/norm/gate/up/down as ONE persistent launch (qz_mlp_chain)")
+                launches.append(n + 1)
                 return y
         xo = q.view(1, 1, H) if shards == 1 else x          # o_proj reads the (gathered) attention output
         a = gemv_4bit(xo, w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1)[:Hs])
@@ -617,9 +621,12 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
             g_, u_ = gemv_4bit_grouped(xa, [(*w["gate"], None, 0, gu_out[0]), (*w["up"], None, 0, gu_out[1])],
                                        exact_codes=True, norm=(nw2, 1e-5))
             h = silu_mul(g_, u_)
-            forms.add("gate/up grouped + silu_mul")
+            forms.add("gate/up " + LAST_FORM.get("grouped", "?") + " + silu_mul")
+            n += 3 if LAST_FORM.get("grouped", "").startswith("norm launch") else 2
         else:
-            forms.add("gate/up pair")
+            forms.add("gate/up " + LAST_FORM.get("pair", "?"))
+            n += 2 if LAST_FORM.get("pair", "").startswith("norm launch") else 1
+        launches.append(n + 2)   # + o_proj, down_proj
         xh = h if shards == 1 else full_h                   # ... the gathered h
         y = gemv_4bit(xh, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1)[:Hs])
         return y if shards == 1 else x
@@ -666,7 +673,7 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
                     f"{layers} layers over {copies} rotating weight sets"
                     + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
             "model": model_name, "shards": shards, "gate_up_form": sorted(forms),
-            "launches_per_layer": 2 if any("ONE persistent" in f for f in forms) else 4,
+            "launches_per_layer": max(launches) if launches else None,
             "chain_barrier_gave_up": failed,
             "us_per_layer": round(us, 3), "algorithmic_bytes_per_layer": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),

@@ -447,6 +447,11 @@ def gemv_4bit(A: Tensor, B: Tensor, out: Optional[Tensor] = None, transposed_A=F
     return out
 
 
+# how the last gemv_4bit_pair_silu / gemv_4bit_grouped call ran (launch forms, for bench.py's
+# chain_roofline line): "pair" / "pair (norm fused)" / "norm launch + pair", "grouped" / ...
+LAST_FORM = {}
+
+
 def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> Optional[Tensor]:
     """F.silu(gate) * up for items = [(B, state, bias[, block_base])] of gate_proj and up_proj
     (equal shapes; block_base for row shards, parallel.sharded_silu_pair) and a single-token A,
@@ -475,12 +480,24 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     if nw is not None and not (nw.dtype == A.dtype and nw.is_cuda and nw.is_contiguous() and nw.numel() == K):
         return None
     bs2 = int(s0.state2.blocksize) if s0.nested else 0
-    rc = lib.qz_gemv_4bit_pair_silu(ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype),
-                                    _gemv_quant_type(s0.quant_type, exact_codes, A.dtype), s0.blocksize, bs2, 0,
-                                    ptr(nw), float(eps), ptr(h), _lib.stream_of(A))
+    qt = _gemv_quant_type(s0.quant_type, exact_codes, A.dtype)
+    rc = lib.qz_gemv_4bit_pair_silu(ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype), qt,
+                                    s0.blocksize, bs2, 0, ptr(nw), float(eps), ptr(h), _lib.stream_of(A))
+    form = "pair" if nw is None else "pair (norm fused)"
+    if rc == _lib.QZ_ERR_SHAPE and nw is not None:
+        # the fused norm is not taken here (the split pair at K = 8192, or too many workgroups to
+        # repeat the norm prologue in): the norm launch, then the pair on its output -- the same
+        # bits as norm -> grouped -> silu_mul.  (Where the pair declines both, that norm launch is
+        # wasted and the caller runs its own.)
+        from .layer_ops import rms_norm
+        A = rms_norm(A, nw, eps).contiguous()
+        rc = lib.qz_gemv_4bit_pair_silu(ctypes.cast(segs, ctypes.c_void_p), K, ptr(A), dtype_code(A.dtype), qt,
+                                        s0.blocksize, bs2, 0, None, 0.0, ptr(h), _lib.stream_of(A))
+        form = "norm launch + pair"
     if rc == _lib.QZ_ERR_SHAPE:
         return None
     check(rc, "gemv_4bit_pair_silu")
+    LAST_FORM["pair"] = form
     return h
 
 
@@ -591,9 +608,11 @@ def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None, norm
                                                   bs2, 0, ptr(nw), float(eps), _lib.stream_of(A))
             if rc != _lib.QZ_ERR_SHAPE:
                 check(rc, "gemv_4bit_grouped(norm)")
+                LAST_FORM["grouped"] = "grouped (norm fused)"
                 return outs
         from .layer_ops import rms_norm
         A = rms_norm(A, nw, eps).contiguous()   # shapes the fused launch does not take: two launches
+    LAST_FORM["grouped"] = "grouped" if norm is None else "norm launch + grouped"
     check(lib.qz_gemv_4bit_grouped(len(items), segp, K, ptr(A), dtype_code(A.dtype), qt, s0.blocksize, bs2, 0,
                                    _lib.stream_of(A)),
           "gemv_4bit_grouped")

@@ -56,7 +56,7 @@ static Knobs read_knobs() {
   k.pair_r = (pr == 2 || pr == 3 || pr == 4 || pr == 6 || pr == 8) ? pr : 0;
   k.pair_wt = env_int("QZ_PAIR_WT", 1) != 0;
   k.pair_ps = env_int("QZ_PAIR_PS", -1);
-  k.pair_wk1 = env_int("QZ_PAIR_WK1", 1) != 0;
+  k.pair_wk1 = env_int("QZ_PAIR_WK1", 0) != 0;
   return k;
 }
 static Knobs g_knobs = read_knobs();   // at library load
@@ -89,6 +89,16 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
   gemv_body<DQ, DT, R, 1, 4, true, CL, WT, NRM, true, TWO, PS>(seg, blockIdx.x, g.seg);
+}
+
+// The split pair (gemv_body PAIR, WK = 2): R rows of gate (waves 0-1) and of up (waves 2-3), each
+// row's K split over two waves as the grouped launch splits it at K = 8192 -- the same bits as that
+// launch + k_silu_mul, in one launch
+template <bool DQ, int DT, bool CL>
+__global__ __launch_bounds__(256) void k_gemv_4bit_pair_split(GemvGroup g) {
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+  const GemvParams seg = g.seg[wave >> 1];
+  gemv_body<DQ, DT, 4, 2, 4, true, CL, false, false, true, false, false>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -414,13 +424,35 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   if (norm_weight && (K % 8 != 0 || K > 16384 || ((uintptr_t)x | (uintptr_t)norm_weight) % 16 != 0))
     return QZ_ERR_SHAPE;
   // the geometry qz_gemv_4bit_grouped takes for the pair's 2M rows (same per-row summation order,
-  // so the same bits); the epilogue needs whole rows per wave, so where the grouped launch splits K
-  // over two waves (WK = 2: the K = 8192 layers of Llama-3-70B) the pair keeps the rows whole
-  // (WK = 1, same R: a different fp32 summation order from the grouped launch there, the same
-  // products).  Single-row waves (R = 1: small row shards, e.g. Llama-3-8B gate/up over 8 ranks)
-  // take the pair launch too
+  // so the same bits).  Where the grouped launch splits K over two waves (R = 4, WK = 2: the K = 8192
+  // layers of Llama-3-70B) the split pair takes it without a norm (with one: QZ_ERR_SHAPE, the caller
+  // normalises first); QZ_PAIR_WK1=1 keeps whole rows per wave there instead (WK = 1, same R: a
+  // different fp32 summation order from the grouped launch, the same products; slower).  Single-row
+  // waves (R = 1: small row shards, e.g. Llama-3-8B gate/up over 8 ranks) take the pair launch too
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
+  if (WK == 2 && R == 4 && !norm_weight && !gemv_knobs().pair_wk1 && !gemv_knobs().pair_r) {
+    // the split pair: the grouped launch's geometry and reduction, bit-identical to it + k_silu_mul
+    // (with a norm the caller runs the norm launch first: 7168 workgroups repeating the norm
+    // prologue cost more than the separate launch, profiles/r3_prenorm_launch_times.txt)
+    GemvGroup gs = g;
+    for (int i = 2; i < kMaxSeg; ++i) gs.start[i] = 0;
+    const unsigned blocks = (unsigned)((M + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == QZ_DT_F16) {
+      if (dq) {
+        if (cl) hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_F16, true>), dim3(blocks), dim3(256), 0, st, gs);
+        else hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_F16, false>), dim3(blocks), dim3(256), 0, st, gs);
+      } else {
+        if (cl) hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_F16, true>), dim3(blocks), dim3(256), 0, st, gs);
+        else hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_F16, false>), dim3(blocks), dim3(256), 0, st, gs);
+      }
+    } else {
+      if (dq) hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_BF16, false>), dim3(blocks), dim3(256), 0, st, gs);
+      else hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_BF16, false>), dim3(blocks), dim3(256), 0, st, gs);
+    }
+    return QZ_OK;
+  }
   if (WK != 1 && !gemv_knobs().pair_wk1) return QZ_ERR_SHAPE;
   WK = 1;
   if (gemv_knobs().pair_r) R = gemv_knobs().pair_r;   // knob; the per-row sums do not depend on R

@@ -88,6 +88,78 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, con
   }
 }
 
+// k_rmsnorm's VEC arithmetic for rows of at most 2048 vectors (K <= 16384 at 16 bits, 8192 at fp32):
+// every thread's vectors of x (and r) and of the weight are loaded up front and held in registers,
+// so a row costs one memory round trip before the reduction instead of one per loop iteration and
+// pass (the Llama-3-70B norm, K = 8192: 8.3 us as the loop, profiles/r5_pair_k8192_ab.txt).  Same
+// per-thread element order, same reduction, same roundings: bit-identical to k_rmsnorm.
+template <int DT, bool ADD>
+__global__ __launch_bounds__(256) void k_rmsnorm_held(const void *__restrict__ x, const void *__restrict__ r, int K,
+                                                      long long ldx, const void *__restrict__ w, float eps,
+                                                      void *__restrict__ y, void *__restrict__ sum, long long ldy) {
+  constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
+  constexpr int V = 16 / ES;
+  constexpr int NC = 8;
+  __shared__ float s_part[4];
+  const long long row = blockIdx.x;
+  const uint4 *xr = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(x) + row * ldx * ES);
+  const uint4 *rr = ADD ? reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(r) + row * ldx * ES) : nullptr;
+  const uint4 *wr = reinterpret_cast<const uint4 *>(w);
+  uint4 *yr = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(y) + row * ldy * ES);
+  uint4 *sr = ADD ? reinterpret_cast<uint4 *>(reinterpret_cast<char *>(sum) + row * ldy * ES) : nullptr;
+  const int nv = K / V;
+  uint4 xa[NC], ra[ADD ? NC : 1], wa[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = (int)threadIdx.x + 256 * c;
+    if (i < nv) {
+      xa[c] = xr[i];
+      if constexpr (ADD) ra[c] = rr[i];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = (int)threadIdx.x + 256 * c;
+    if (i < nv) wa[c] = wr[i];
+  }
+  float h[NC][V];
+  float ss = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if ((int)threadIdx.x + 256 * c < nv) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float xe = load_f32<DT>(&xa[c], j);
+        if constexpr (ADD) h[c][j] = round_dt<DT>(__fadd_rn(load_f32<DT>(&ra[c < (ADD ? NC : 1) ? c : 0], j), xe));
+        else h[c][j] = xe;
+        ss = __fadd_rn(ss, __fmul_rn(h[c][j], h[c][j]));
+      }
+    }
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = __fadd_rn(__fadd_rn(s_part[0], s_part[1]), __fadd_rn(s_part[2], s_part[3]));
+  const float rs = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)K), eps));
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = (int)threadIdx.x + 256 * c;
+    if (i < nv) {
+      uint4 ov, sv;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if constexpr (ADD) store_f32<DT>(&sv, j, h[c][j]);
+        const float hn = round_dt<DT>(__fmul_rn(h[c][j], rs));
+        float o = __fmul_rn(load_f32<DT>(&wa[c], j), hn);
+        asm volatile("" : "+v"(o));
+        store_f32<DT>(&ov, j, o);
+      }
+      if constexpr (ADD) sr[i] = sv;
+      yr[i] = ov;
+    }
+  }
+}
+
 struct RopeArgs {
   const void *x[2];
   void *o[2];
@@ -135,6 +207,26 @@ __global__ __launch_bounds__(256) void k_silu_mul(const void *__restrict__ g, co
   const float x = load_f32<DT>(g, i);
   const float a = round_dt<DT>(__fdiv_rn(x, __fadd_rn(1.0f, expf(-x))));
   store_f32<DT>(y, i, __fmul_rn(a, load_f32<DT>(u, i)));
+}
+
+// k_silu_mul on 16-B vectors (n a multiple of the vector, 16-B aligned operands): the same
+// per-element arithmetic, one load of each operand per thread
+template <int DT>
+__global__ __launch_bounds__(256) void k_silu_mul_vec(const void *__restrict__ g, const void *__restrict__ u,
+                                                      long long nvec, void *__restrict__ y) {
+  constexpr int V = DT == QZ_DT_F32 ? 4 : 8;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nvec) return;
+  const uint4 gv = reinterpret_cast<const uint4 *>(g)[i];
+  const uint4 uv = reinterpret_cast<const uint4 *>(u)[i];
+  uint4 ov;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const float x = load_f32<DT>(&gv, j);
+    const float a = round_dt<DT>(__fdiv_rn(x, __fadd_rn(1.0f, expf(-x))));
+    store_f32<DT>(&ov, j, __fmul_rn(a, load_f32<DT>(&uv, j)));
+  }
+  reinterpret_cast<uint4 *>(y)[i] = ov;
 }
 
 // ---------------------------------------------------------------------------
@@ -451,7 +543,10 @@ template <int DT, bool ADD>
 void launch_rmsnorm(bool vec, long long rows, const void *x, const void *r, int K, long long ldx, const void *w,
                     float eps, void *y, void *sum, long long ldy, hipStream_t s) {
   const dim3 g((unsigned)rows), b(256);
-  if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
+  constexpr int V = DT == QZ_DT_F32 ? 4 : 8;
+  if (vec && K / V <= 256 * 8)
+    hipLaunchKernelGGL((k_rmsnorm_held<DT, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
+  else if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
   else hipLaunchKernelGGL((k_rmsnorm<DT, false, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
 }
 
@@ -535,6 +630,18 @@ extern "C" int qz_silu_mul(const void *gate, const void *up, int dtype, long lon
   const long long blocks = (n + 255) / 256;
   if (blocks > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
+  const int v = dtype == QZ_DT_F32 ? 4 : 8;
+  if (n % v == 0 && ((uintptr_t)gate | (uintptr_t)up | (uintptr_t)y) % 16 == 0) {
+    const long long nvec = n / v;
+    const dim3 gv((unsigned)((nvec + 255) / 256)), bv(256);
+    switch (dtype) {
+      case QZ_DT_F16: hipLaunchKernelGGL((k_silu_mul_vec<QZ_DT_F16>), gv, bv, 0, s, gate, up, nvec, y); break;
+      case QZ_DT_BF16: hipLaunchKernelGGL((k_silu_mul_vec<QZ_DT_BF16>), gv, bv, 0, s, gate, up, nvec, y); break;
+      case QZ_DT_F32: hipLaunchKernelGGL((k_silu_mul_vec<QZ_DT_F32>), gv, bv, 0, s, gate, up, nvec, y); break;
+      default: return QZ_ERR_DTYPE;
+    }
+    return (int)hipGetLastError();
+  }
   const dim3 grid((unsigned)blocks), blk(256);
   switch (dtype) {
     case QZ_DT_F16: hipLaunchKernelGGL((k_silu_mul<QZ_DT_F16>), grid, blk, 0, s, gate, up, n, y); break;

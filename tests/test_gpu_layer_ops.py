@@ -42,7 +42,8 @@ def _ulp_at(y, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("shape", [(1, 1, 4096), (2, 7, 4096), (3, 5, 1000), (1, 1, 8192), (4096, 256)])
+@pytest.mark.parametrize("shape", [(1, 1, 4096), (2, 7, 4096), (3, 5, 1000), (1, 1, 8192), (4096, 256),
+                                   (1, 1, 16384), (2, 1, 16392)])   # the register-held kernel's limit, past it
 def test_rms_norm_vs_llama_rmsnorm(dtype, shape):
     from quantizations_amd.layer_ops import rms_norm
 
@@ -102,7 +103,7 @@ def test_rope_qk_bit_exact_vs_apply_rotary_pos_emb(dtype, B, Hq, Hk, S, D, bcast
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("shape", [(1, 1, 14336), (4, 1, 14336), (2, 9, 1000), (3, 333)])
+@pytest.mark.parametrize("shape", [(1, 1, 14336), (4, 1, 14336), (2, 9, 1000), (3, 333), (1, 1, 28672), (1, 1, 36)])
 def test_silu_mul_vs_torch(dtype, shape):
     from quantizations_amd.layer_ops import silu_mul
 
@@ -114,6 +115,19 @@ def test_silu_mul_vs_torch(dtype, shape):
     d = (y.double() - ref.double()).abs()
     assert bool((d <= 2 * _ulp_at(ref, dtype) + 1e-30).all()), float(d.max())
     assert (y == ref).float().mean().item() >= 0.99
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_silu_mul_vector_and_scalar_kernels_agree(dtype):
+    """16-B aligned operands take the vector kernel, an offset view the per-element one: same bits."""
+    from quantizations_amd.layer_ops import silu_mul
+
+    n = 28672
+    g = (torch.randn(n + 1, device=DEV) * 4).to(dtype)
+    u = (torch.randn(n + 1, device=DEV) * 4).to(dtype)
+    a = silu_mul(g[1:], u[1:])              # 2- or 4-byte offset: scalar kernel
+    b = silu_mul(g[1:].clone(), u[1:].clone())
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)

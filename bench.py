@@ -545,7 +545,7 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 @torch.inference_mode()
 def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b",
-                   mlp_chain: bool = False, prefetch=None):
+                   mlp_chain: bool = False):
     """The Linear4bit chain of a Llama-3 decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
@@ -560,11 +560,9 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     norm, gate/up + SiLU and down_proj + residual as the ONE persistent launch the product runs
     (core.gemv_4bit_mlp_chain), so a layer is two launches.  shards = P > 1: the same chain on ONE rank's
     rows of the row-split layout (every projection M / P rows, the launches a rank runs per layer
-    at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6.
-    prefetch = (workgroups, depth): a side stream streams layer L + 1's weights into the Infinity
-    Cache (core.prefetch_l3) while layer L computes."""
+    at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
     from quantizations_amd.core import (LAST_FORM, gemv_4bit, gemv_4bit_grouped, gemv_4bit_mlp_chain,
-                                        gemv_4bit_pair_silu, mlp_chain_state, prefetch_l3, quantize_4bit)
+                                        gemv_4bit_pair_silu, mlp_chain_state, quantize_4bit)
     from quantizations_amd.layer_ops import silu_mul
 
     base_cfg = MODELS[model_name]
@@ -633,27 +631,10 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
         y = gemv_4bit(xh, w["down"][0], state=w["down"][1], exact_codes=True, residual=a.view(-1)[:Hs])
         return y if shards == 1 else x
 
-    side = torch.cuda.Stream() if prefetch else None
-
-    def wlist(w):
-        out = []
-        for pk, st in w.values():
-            out += [pk, st.absmax, st.state2.absmax if st.nested else None]
-        return out
-
     def chain():
         x = x0
-        main = torch.cuda.current_stream()
         for i in range(layers):
-            if side is not None:
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
-                with torch.cuda.stream(side):
-                    prefetch_l3(wlist(sets[(i + 1) % copies]), workgroups=prefetch[0], depth=prefetch[1])
             x = layer(x, sets[i % copies])
-        if side is not None:
-            main.wait_stream(side)
         return x
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -692,7 +673,6 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
                     f"{layers} layers over {copies} rotating weight sets"
                     + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
             "model": model_name, "shards": shards, "gate_up_form": sorted(forms),
-            "l3_prefetch": list(prefetch) if prefetch else None,
             "launches_per_layer": max(launches) if launches else None,
             "chain_barrier_gave_up": failed,
             "us_per_layer": round(us, 3), "algorithmic_bytes_per_layer": nbytes,

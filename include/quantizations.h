@@ -303,13 +303,6 @@ int qz_rope_qk(int dtype, int B, int S, int D, const void *q, int Hq, const long
  * contiguous elements of `dtype` (torch's two rounded elementwise ops). */
 int qz_silu_mul(const void *gate, const void *up, int dtype, long long n, void *y, void *stream);
 
-/* Warms the die-level Infinity Cache with up to 16 byte ranges (ptrs[i], bytes[i]): every aligned
- * 16-B piece is loaded once and discarded (csrc/prefetch.hip).  For a decode step's NEXT weights on a
- * side stream while the current launches compute; writes nothing the caller reads (sink: >= 64 words
- * of scratch).  workgroups 0 = 2 per CU; depth 0 (= 8), 4, 8 or 16 pieces in flight per lane.  No
- * reference counterpart (the reference streams weights from HBM in every launch). */
-int qz_prefetch_l3(int nseg, const void *const *ptrs, const long long *bytes, int workgroups, int depth,
-                   unsigned int *sink, void *stream);
 
 /* One new token of LlamaAttention.forward (modeling_llama.py:243-281) against a static KV
  * cache, from the q/k/v projection outputs to the o_proj input, in one launch (two when

@@ -501,28 +501,6 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     return h
 
 
-_PREFETCH_SINK = {}
-
-
-def prefetch_l3(tensors, workgroups: int = 0, depth: int = 0) -> None:
-    """Warm the Infinity Cache with `tensors`' bytes (qz_prefetch_l3: every aligned 16-B piece loaded
-    once, nothing written) on the current stream -- a decode step's NEXT weights, from a side
-    stream.  Up to 16 tensors per call (more: several launches)."""
-    ts = [t for t in tensors if t is not None and t.numel() > 0]
-    if not ts:
-        return
-    dev = ts[0].device
-    sink = _PREFETCH_SINK.get(dev)
-    if sink is None:
-        sink = _PREFETCH_SINK[dev] = torch.zeros(64, dtype=torch.int32, device=dev)
-    for i in range(0, len(ts), 16):
-        chunk = ts[i:i + 16]
-        ptrs = (ctypes.c_void_p * len(chunk))(*[t.data_ptr() for t in chunk])
-        nbytes = (ctypes.c_longlong * len(chunk))(*[t.numel() * t.element_size() for t in chunk])
-        check(lib.qz_prefetch_l3(len(chunk), ptrs, nbytes, int(workgroups), int(depth), ptr(sink),
-                                 _lib.stream_of(chunk[0])), "prefetch_l3")
-
-
 def mlp_chain_state(device) -> Tensor:
     """Sync state of qz_mlp_chain (int32 words, zeroed once; one per stream running chains)."""
     return torch.zeros(int(lib.qz_mlp_chain_state_words()), dtype=torch.int32, device=device)

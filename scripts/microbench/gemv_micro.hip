@@ -3,7 +3,7 @@
 // Infinity Cache never serves repeats.  Printed numbers are hipEvent back-to-back averages
 // (kernel + launch gap) over interleaved rounds; `stamps` prints in-kernel wave timelines.
 //
-//   gemv_micro M K [rounds] [geom|stamps]
+//   gemv_micro M K [rounds] [geom|geom8k|stamps]
 //
 // The losing experiment variants of rounds 1-4 (register v_perm decodes, MFMA decodes, the
 // streaming form, step rings, next-launch prefetch, ablation bits) were removed from the product
@@ -114,6 +114,12 @@ int main(int argc, char **argv) {
     }
     GV(2, 1, 4, true, false, false); GV(4, 1, 4, true, false, false); GV(4, 2, 4, true, false, false);
     GV(2, 1, 8, true, true, false); GV(4, 1, 8, true, true, false); GV(2, 1, 4, false, false, false);
+  }
+  if (mode == "geom8k") {  // K = 8192 (Llama-3-70B q/k/v, o, gate/up): K split over 2 / 4 waves, 8-wave tables
+    GV(4, 2, 4, true, false, false); GV(2, 2, 4, true, false, false); GV(1, 2, 4, true, false, false);
+    GV(2, 4, 4, true, false, false); GV(4, 4, 4, true, false, false); GV(4, 1, 4, true, false, false);
+    GV(2, 1, 4, true, false, false); GV(4, 2, 8, true, true, false); GV(2, 2, 8, true, true, false);
+    GV(4, 1, 8, true, true, false); GV(2, 1, 8, true, true, false); GV(4, 4, 8, true, true, false);
   }
   if (mode == "stamps") {  // timeline of one steady-state launch (the last of 30 back-to-back), 12 samples each
     const int NWAVES = 1 << 16;

@@ -56,7 +56,7 @@ static Knobs read_knobs() {
   k.pair_r = (pr == 2 || pr == 3 || pr == 4 || pr == 6 || pr == 8) ? pr : 0;
   k.pair_wt = env_int("QZ_PAIR_WT", 1) != 0;
   k.pair_ps = env_int("QZ_PAIR_PS", -1);
-  k.pair_wk1 = env_int("QZ_PAIR_WK1", 0) != 0;
+  k.pair_wk1 = env_int("QZ_PAIR_WK1", 1);
   return k;
 }
 static Knobs g_knobs = read_knobs();   // at library load
@@ -89,16 +89,6 @@ __global__ __launch_bounds__(256) void k_gemv_4bit_pair(GemvGroup g) {
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
   const GemvParams seg = g.seg[wave >> 1];
   gemv_body<DQ, DT, R, 1, 4, true, CL, WT, NRM, true, TWO, PS>(seg, blockIdx.x, g.seg);
-}
-
-// The split pair (gemv_body PAIR, WK = 2): R rows of gate (waves 0-1) and of up (waves 2-3), each
-// row's K split over two waves as the grouped launch splits it at K = 8192 -- the same bits as that
-// launch + k_silu_mul, in one launch
-template <bool DQ, int DT, bool CL>
-__global__ __launch_bounds__(256) void k_gemv_4bit_pair_split(GemvGroup g) {
-  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
-  const GemvParams seg = g.seg[wave >> 1];
-  gemv_body<DQ, DT, 4, 2, 4, true, CL, false, false, true, false, false>(seg, blockIdx.x, g.seg);
 }
 
 // Generic path for shapes the vector kernel does not cover (K % 32 != 0,
@@ -305,6 +295,10 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   // QZ_GROUPED_NORM_R (knob): rows per wave of the fused pre-norm launch where the geometry keeps
   // whole rows per wave (WK = 1: the same per-row sums)
   if (nw && gemv_knobs().norm_r && WK == 1) R = gemv_knobs().norm_r;
+  // where K is split over waves (K = 8192: the Llama-3-70B q/k/v) the norm launch + the plain grouped
+  // launch beat the fused prologue, repeated by 1280 small workgroups (16.41 vs 17.23 us,
+  // profiles/r5_qkv70_forms.txt): the caller runs the two launches
+  if (nw && WK != 1) return QZ_ERR_SHAPE;
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -424,37 +418,21 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   if (norm_weight && (K % 8 != 0 || K > 16384 || ((uintptr_t)x | (uintptr_t)norm_weight) % 16 != 0))
     return QZ_ERR_SHAPE;
   // the geometry qz_gemv_4bit_grouped takes for the pair's 2M rows (same per-row summation order,
-  // so the same bits).  Where the grouped launch splits K over two waves (R = 4, WK = 2: the K = 8192
-  // layers of Llama-3-70B) the split pair takes it without a norm (with one: QZ_ERR_SHAPE, the caller
-  // normalises first); QZ_PAIR_WK1=1 keeps whole rows per wave there instead (WK = 1, same R: a
-  // different fp32 summation order from the grouped launch, the same products; slower).  Single-row
-  // waves (R = 1: small row shards, e.g. Llama-3-8B gate/up over 8 ranks) take the pair launch too
+  // so the same bits where it keeps whole rows per wave).  Single-row waves (R = 1: small row shards,
+  // e.g. Llama-3-8B gate/up over 8 ranks) take the pair launch too
   int R, WK;
   choose_geometry(2 * M, K, dtype, &R, &WK);
-  if (WK == 2 && R == 4 && !norm_weight && !gemv_knobs().pair_wk1 && !gemv_knobs().pair_r) {
-    // the split pair: the grouped launch's geometry and reduction, bit-identical to it + k_silu_mul
-    // (with a norm the caller runs the norm launch first: 7168 workgroups repeating the norm
-    // prologue cost more than the separate launch, profiles/r3_prenorm_launch_times.txt)
-    GemvGroup gs = g;
-    for (int i = 2; i < kMaxSeg; ++i) gs.start[i] = 0;
-    const unsigned blocks = (unsigned)((M + 3) / 4);
-    hipStream_t st = (hipStream_t)stream;
-    if (dtype == QZ_DT_F16) {
-      if (dq) {
-        if (cl) hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_F16, true>), dim3(blocks), dim3(256), 0, st, gs);
-        else hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_F16, false>), dim3(blocks), dim3(256), 0, st, gs);
-      } else {
-        if (cl) hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_F16, true>), dim3(blocks), dim3(256), 0, st, gs);
-        else hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_F16, false>), dim3(blocks), dim3(256), 0, st, gs);
-      }
-    } else {
-      if (dq) hipLaunchKernelGGL((k_gemv_4bit_pair_split<true, QZ_DT_BF16, false>), dim3(blocks), dim3(256), 0, st, gs);
-      else hipLaunchKernelGGL((k_gemv_4bit_pair_split<false, QZ_DT_BF16, false>), dim3(blocks), dim3(256), 0, st, gs);
-    }
-    return QZ_OK;
+  if (WK != 1) {
+    // K split over waves in the grouped launch (the K = 8192 layers of Llama-3-70B; small pairs):
+    // the pair keeps whole rows per wave -- the same products in another fp32 summation order
+    // (faster: 28672 x 8192 gate/up 52-55 us against 57-59 for the grouped launch and 60-61 for a
+    // split-K pair, profiles/r5_pair_k8192_forms.txt).  Without the norm: with it (7168 workgroups
+    // each normalising 16 KiB of x) the pair took 70.8 us, so QZ_ERR_SHAPE and the caller runs the
+    // norm launch first (QZ_PAIR_WK1=2 fuses it anyway; 0 declines these geometries altogether)
+    const int wk1 = gemv_knobs().pair_wk1;
+    if (wk1 == 0 || (norm_weight && wk1 != 2)) return QZ_ERR_SHAPE;
+    WK = 1;
   }
-  if (WK != 1 && !gemv_knobs().pair_wk1) return QZ_ERR_SHAPE;
-  WK = 1;
   if (gemv_knobs().pair_r) R = gemv_knobs().pair_r;   // knob; the per-row sums do not depend on R
   const int blocks = (M + 2 * R - 1) / (2 * R);
   if (norm_weight && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
@@ -544,7 +522,7 @@ extern "C" int qz_gemv_set_knob(const char *name, int value) {
   else if (!strcmp(name, "QZ_PAIR_R")) k.pair_r = (value == 2 || value == 3 || value == 4 || value == 6 || value == 8) ? value : 0;
   else if (!strcmp(name, "QZ_PAIR_WT")) k.pair_wt = value != 0;
   else if (!strcmp(name, "QZ_PAIR_PS")) k.pair_ps = value;
-  else if (!strcmp(name, "QZ_PAIR_WK1")) k.pair_wk1 = value != 0;
+  else if (!strcmp(name, "QZ_PAIR_WK1")) k.pair_wk1 = value;
   else return QZ_ERR_ARG;
   return QZ_OK;
 }

@@ -590,8 +590,7 @@ template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, boo
           int STAMP = 0>
 __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block, const GemvParams *pair = nullptr) {
   static_assert(!NRM || (NW == 4 && FS && DT != QZ_DT_F32), "fused pre-norm: 4 waves, full steps, 16-bit activations");
-  static_assert(!PAIR || (NW == 4 && (WK == 1 || (WK == 2 && !NRM && !TWO && !PS)) && DT != QZ_DT_F32),
-                "pair: 4 waves, WK = 1 (or the split form: WK = 2, no norm), 16-bit activations");
+  static_assert(!PAIR || (NW == 4 && WK == 1 && DT != QZ_DT_F32), "pair: 4 waves, WK = 1, 16-bit activations");
   static_assert(!PS || (PAIR && FS), "persistent form: pair launches, full steps");
   static_assert(!TWO || (FS && WK == 1), "two-step form: full steps, whole rows per wave");
   static_assert(!CL || DT == QZ_DT_F16, "exact codes are the fp16-activation table");
@@ -616,7 +615,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int wk = wave % WK;
   const int rg = wave / WK;
-  int row0 = PAIR ? (WK == 1 ? (block * 2 + (wave & 1)) * R : block * R) : (block * RG + rg) * R;
+  int row0 = PAIR ? (block * 2 + (wave & 1)) * R : (block * RG + rg) * R;
   const int cb = PAIR ? (wave >> 1) : 0;   // this wave's code2 table
   const int row_bytes = p.K >> 1;
   const int nsteps = (row_bytes + 1023) >> 10;
@@ -874,37 +873,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
   }
 
   QZ_STAMP(3);
-  if constexpr (PAIR && WK == 2) {
-    // the split pair: waves 0-1 hold the two K-halves of gate's R rows, waves 2-3 those of up's.
-    // Each projection is reduced exactly as the grouped WK = 2 launch reduces it (0 + part 0 +
-    // part 1, then the output scale and the bias), then k_silu_mul's arithmetic
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float v = wave_sum_last(acc[r]);
-      if (lane == kWave - 1) s_part[wave][r] = v;
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < R) {
-      const int r = threadIdx.x;
-      const int row = block * R + r;
-      if (row < p.M) {
-        float pv[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float v = 0.0f;
-#pragma unroll
-          for (int k = 0; k < 2; ++k) v += s_part[2 * j + k][r];
-          v *= out_scale;
-          const void *bias = keep_sp(pair[j].bias);
-          if (bias) v += load_f32<DT>(bias, row);
-          pv[j] = round_store<DT>(v);
-        }
-        const float a = round_store<DT>(__fdiv_rn(pv[0], __fadd_rn(1.0f, expf(-pv[0]))));
-        store_f32<DT>(keep_sp(pair[0].y), row, __fmul_rn(a, pv[1]));
-      }
-    }
-    return;
-  } else if constexpr (PAIR) {  // gate (waves 0-1) and up (waves 2-3) of the same rows meet in LDS
+  if constexpr (PAIR) {  // gate (waves 0-1) and up (waves 2-3) of the same rows meet in LDS
     float v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = wave_sum_last(acc[r]);
@@ -1001,9 +970,10 @@ struct Knobs {
   int pair_r;   // QZ_PAIR_R=2|3|4|6|8: rows per wave of the pair launch (0 = geometry's)
   int pair_wt;  // QZ_PAIR_WT=0: the persistent pair keeps the 16-copy exact table (default 1)
   int pair_ps;  // QZ_PAIR_PS: 0 = one workgroup per block, 1..8 = workgroups per CU, >= 16 = the grid; -1 = default
-  int pair_wk1; // QZ_PAIR_WK1=1: where the grouped geometry splits K over two waves (K = 8192), the pair launch
-                // keeps whole rows per wave (norm fused; measured slower on Llama-3-70B: 91.7 vs 95.9 tok/s,
-                // profiles/r5_pair_k8192_ab.txt); default 0: the split pair (R = 4, WK = 2, no norm)
+  int pair_wk1; // QZ_PAIR_WK1: where the grouped geometry splits K over waves (K = 8192), the pair launch
+                // 1 (default): keeps whole rows per wave, without a fused norm (with one: declines, the caller
+                // runs the norm launch first); 2: fuses the norm there too (slower: 70B 91.7 vs 95.9 tok/s,
+                // profiles/r5_pair_k8192_ab.txt); 0: declines (round 4: grouped launch + SiLU launch)
 };
 // the knobs the library read at load (gemv.hip); qz_gemv_set_knob changes one explicitly
 Knobs &gemv_knobs();

@@ -10,6 +10,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "scripts", "dev"))
 from pair_ps_times_lib import graph_time  # noqa: E402
 from test_gpu_prenorm import _items, DEV  # noqa: E402
 from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu  # noqa: E402
@@ -31,3 +32,15 @@ t_si = graph_time(lambda i: silu_mul(gate, up))
 t_nm = graph_time(lambda i: rms_norm(x, w, 1e-5))
 print(f"{M}x{K} gate/up: grouped {t_gr:.2f} us, split pair {t_pr:.2f} us, silu_mul {t_si:.2f} us, "
       f"rms_norm(K={K}) {t_nm:.2f} us (b2b in one graph)", flush=True)
+# whole rows per wave (QZ_PAIR_WK1=1) without the norm, one workgroup per block, R = 4 / 2 / 8
+from quantizations_amd import _lib  # noqa: E402
+_lib.set_gemv_knob("QZ_PAIR_WK1", 1)
+for r in (4, 2, 8):
+    _lib.set_gemv_knob("QZ_PAIR_R", r)
+    for ps in (0, 2, 3):
+        _lib.set_gemv_knob("QZ_PAIR_PS", ps)
+        t = graph_time(lambda i: gemv_4bit_pair_silu(x, copies[i % NC], exact_codes=True))
+        print(f"whole-row pair R={r} QZ_PAIR_PS={ps}: {t:.2f} us", flush=True)
+_lib.set_gemv_knob("QZ_PAIR_WK1", 0)
+_lib.set_gemv_knob("QZ_PAIR_R", 0)
+_lib.set_gemv_knob("QZ_PAIR_PS", -1)

@@ -21,7 +21,7 @@ def knobs():
     from quantizations_amd import _lib
 
     yield _lib.set_gemv_knob
-    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0), ("QZ_PAIR_WK1", 0)):
+    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0), ("QZ_PAIR_WK1", 1)):
         _lib.set_gemv_knob(name, v)
 
 
@@ -40,12 +40,7 @@ def _items(M, K, dtype, seed, quant="nf4", dq=True, bias=False):
 
 @pytest.mark.parametrize("dtype,exact", [(torch.float16, True), (torch.float16, None), (torch.bfloat16, None)])
 @pytest.mark.parametrize("M,K,norm,bias", [(14336, 4096, True, False), (14336, 4096, False, False),
-                                           (3000, 2048, True, True), (4096, 6144, False, True),
-                                           # the split pair (K = 8192: R = 4, K over two waves), without
-                                           # and with a norm (run as its own launch first), ragged, and
-                                           # the Llama-3-70B gate/up shape
-                                           (4096, 8192, False, False), (4098, 8192, True, True),
-                                           (28672, 8192, True, False)])
+                                           (3000, 2048, True, True), (4096, 6144, False, True)])
 def test_pair_silu_bit_identical_to_grouped_plus_product(dtype, exact, M, K, norm, bias):
     from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
     from quantizations_amd.layer_ops import silu_mul
@@ -140,38 +135,56 @@ def test_pair_silu_on_row_shards(world, rank):
     assert torch.equal(h.reshape(-1), full.reshape(-1)[r0:r1])
 
 
-@pytest.mark.parametrize("quant,dq", [("fp4", False), ("nf4", False), ("fp4", True)])
-def test_pair_silu_split_other_formats(quant, dq):
-    """The split pair with FP4 codes and fp32 absmax: the grouped launch + product's bits."""
-    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
-    from quantizations_amd.layer_ops import silu_mul
-
-    items = _items(4100, 8192, torch.float16, seed=11, quant=quant, dq=dq)
-    x = torch.randn(1, 1, 8192, device=DEV).half()
-    gate, up = gemv_4bit_grouped(x, items)
-    h = gemv_4bit_pair_silu(x, items)
-    assert h is not None and torch.equal(h, silu_mul(gate, up))
-
-
-@pytest.mark.parametrize("M,K", [(4096, 8192), (1000, 6144)])
-def test_pair_silu_whole_rows_knob(knobs, M, K):
-    """QZ_PAIR_WK1=1: where the grouped launch splits K over two waves (K = 8192; small pairs), the
-    pair keeps whole rows per wave -- the same products in another fp32 summation order, so within
-    fp16 rounding of the grouped launch + product (measured slower on Llama-3-70B, hence off).  By
-    default (1000, 6144) -- R = 1, K split -- is declined: None, nothing launched."""
-    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
-
-    items = _items(M, K, torch.float16, seed=M, quant="nf4")
-    x = torch.randn(1, 1, K, device=DEV).half()
-    gate, up = gemv_4bit_grouped(x, items, exact_codes=True)
+def _rel_to_grouped(h, gate, up):
     ref = F.silu(gate.float()) * up.float()
-    if M == 1000:
-        assert gemv_4bit_pair_silu(x, items, exact_codes=True) is None
-    knobs("QZ_PAIR_WK1", 1)
-    h = gemv_4bit_pair_silu(x, items, exact_codes=True)
+    return ((h.float() - ref).norm() / ref.norm()).item()
+
+
+@pytest.mark.parametrize("M,norm,bias,quant,dq", [
+    (4096, False, False, "nf4", True), (4098, True, True, "nf4", True),    # ragged last block; norm launch first
+    (28672, True, False, "nf4", True),                                     # Llama-3-70B gate/up as decoded
+    (4100, False, False, "fp4", False), (4100, True, False, "nf4", False), (4100, False, True, "fp4", True)])
+def test_pair_silu_whole_rows_at_k8192(knobs, M, norm, bias, quant, dq):
+    """K = 8192, where the grouped launch splits K over two waves: the pair keeps whole rows per wave
+    -- the same products in another fp32 summation order, so within fp16 rounding of the grouped
+    launch + product.  With a norm, the C entry declines the fused prologue and core runs the norm
+    launch, then the pair: bit-identical to norm launch -> pair without norm.  QZ_PAIR_WK1=2 fuses the
+    norm (same bits as norm launch + pair), 0 declines (None, nothing launched)."""
+    from quantizations_amd.core import LAST_FORM, gemv_4bit_grouped, gemv_4bit_pair_silu
+    from quantizations_amd.layer_ops import rms_norm
+
+    K = 8192
+    items = _items(M, K, torch.float16, seed=M, quant=quant, dq=dq, bias=bias)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 2).half()
+    nw = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).half() if norm else None
+    nrm = (nw, 1e-5) if norm else None
+    h = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=nrm)
     assert h is not None
-    rel = ((h.float() - ref).norm() / ref.norm()).item()
-    assert rel < 2e-3, rel
+    assert LAST_FORM["pair"] == ("norm launch + pair" if norm else "pair")
+    xn = rms_norm(x, nw, 1e-5) if norm else x
+    gate, up = gemv_4bit_grouped(xn, items, exact_codes=True)
+    assert _rel_to_grouped(h, gate, up) < 2e-3
+    if norm:
+        assert torch.equal(h, gemv_4bit_pair_silu(xn, items, exact_codes=True))
+        knobs("QZ_PAIR_WK1", 2)
+        h2 = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=nrm)
+        assert LAST_FORM["pair"] == "pair (norm fused)" and torch.equal(h2, h)
+    knobs("QZ_PAIR_WK1", 0)
+    assert gemv_4bit_pair_silu(xn, items, exact_codes=True) is None
+
+
+def test_pair_silu_whole_rows_for_small_k_split_pairs(knobs):
+    """(1000, 6144): R = 1 with K over two waves in the grouped geometry -- whole rows in the pair."""
+    from quantizations_amd.core import gemv_4bit_grouped, gemv_4bit_pair_silu
+
+    items = _items(1000, 6144, torch.float16, seed=1000)
+    x = torch.randn(1, 1, 6144, device=DEV).half()
+    h = gemv_4bit_pair_silu(x, items, exact_codes=True)
+    gate, up = gemv_4bit_grouped(x, items, exact_codes=True)
+    assert h is not None and _rel_to_grouped(h, gate, up) < 2e-3
+    knobs("QZ_PAIR_WK1", 0)
+    assert gemv_4bit_pair_silu(x, items, exact_codes=True) is None
 
 
 def test_pair_silu_declines_what_it_cannot_take():

@@ -44,3 +44,20 @@ for r in (4, 2, 8):
 _lib.set_gemv_knob("QZ_PAIR_WK1", 0)
 _lib.set_gemv_knob("QZ_PAIR_R", 0)
 _lib.set_gemv_knob("QZ_PAIR_PS", -1)
+# with the norm: the norm launch + the whole-row pair (default) against the norm fused into the
+# persistent whole-row pair (QZ_PAIR_WK1=2) on the 16-copy table (QZ_PAIR_WT=0: 3 workgroups per CU
+# fit) or the 256-B-entry one (64 KiB + the 16 KiB image: one workgroup per CU)
+nrm = (w, 1e-5)
+ref = gemv_4bit_pair_silu(x, copies[0], exact_codes=True, norm=nrm)
+t = graph_time(lambda i: gemv_4bit_pair_silu(x, copies[i % NC], exact_codes=True, norm=nrm))
+print(f"norm launch + whole-row pair: {t:.2f} us", flush=True)
+_lib.set_gemv_knob("QZ_PAIR_WK1", 2)
+for wt, ps in ((0, 3), (0, 2), (0, 4), (1, 2), (0, 0)):
+    _lib.set_gemv_knob("QZ_PAIR_WT", wt)
+    _lib.set_gemv_knob("QZ_PAIR_PS", ps)
+    same = torch.equal(gemv_4bit_pair_silu(x, copies[0], exact_codes=True, norm=nrm), ref)
+    t = graph_time(lambda i: gemv_4bit_pair_silu(x, copies[i % NC], exact_codes=True, norm=nrm))
+    print(f"norm fused, whole rows, QZ_PAIR_WT={wt} QZ_PAIR_PS={ps}: {t:.2f} us (same bits: {same})", flush=True)
+_lib.set_gemv_knob("QZ_PAIR_WK1", 1)
+_lib.set_gemv_knob("QZ_PAIR_WT", 1)
+_lib.set_gemv_knob("QZ_PAIR_PS", -1)

@@ -251,6 +251,7 @@ extern "C" int qz_gemv_4bit_residual(int M, int K, const void *x, int dtype, con
 // nw != nullptr: x is first RMSNorm'd with weight nw / epsilon eps, bit-identically to qz_rmsnorm
 // (the pre-norm of q/k/v and gate/up fused into their grouped launch)
 constexpr int kNormMaxBlocks = 4096;
+constexpr size_t kLdsPerCU = 160 * 1024;   // gfx950: LDS per compute unit
 static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
                              int blocksize, int blocksize2, const float *lut, const void *nw, float eps, void *stream) {
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;
@@ -451,14 +452,22 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
   // workgroups per CU: 16.2-16.8 -> 15.1 us for 14336 rows, 10.8 -> 10.6 for 7168
   // (profiles/r4_pair_persistent_wide_table.txt), from 3 blocks per workgroup on (at the N = 4
   // shard, 896 blocks, the 16-copy table at 3 per CU is 3 % faster)
+  // The persistent grid must be resident at once (a second round of persistent workgroups repeats the
+  // whole block loop): workgroups per CU = what the LDS admits -- the byte table (32 KiB, 64 KiB for
+  // the 256-B-entry one), the normalised image (2K bytes) and ~4 KiB of partials -- capped at 3.  At
+  // K = 8192 the wide table + image (84 KiB) fits once, so the wide table is taken only where two fit.
   const int cus = device_cus();
-  const bool wt_ok = cl && norm_weight && (R == 2 || R == 4) && blocks >= 3 * 2 * cus && gemv_knobs().pair_wt;
+  const size_t img = norm_weight ? (size_t)K * 2 : 0;
+  const int per_cu_wt = (int)std::min<size_t>(3, kLdsPerCU / (2 * kTabDwords * 4 + img + 4096));
+  const int per_cu = (int)std::min<size_t>(3, kLdsPerCU / (kTabDwords * 4 + img + 4096));
+  const bool wt_ok = cl && norm_weight && (R == 2 || R == 4) && blocks >= 3 * 2 * cus && per_cu_wt >= 2 &&
+                     gemv_knobs().pair_wt;
   int pgrid_i = 0;
   if (gemv_knobs().pair_ps >= 0) {
     const int ps = gemv_knobs().pair_ps;
     pgrid_i = ps <= 0 ? 0 : ps <= 8 ? cus * ps : ps;
   } else if (norm_weight) {
-    pgrid_i = (wt_ok ? 2 : 3) * cus;
+    pgrid_i = (wt_ok ? 2 : per_cu) * cus;
   }
   const unsigned pgrid = (unsigned)max(pgrid_i, 1);
   const bool persist = pgrid_i > 0 && pgrid_i < blocks;   // the two-step form or the step loop (K != 4096)

@@ -254,6 +254,14 @@ constexpr int kAttnChunk = 128;  // key positions per workgroup
 #endif
 constexpr int kAttnAbl = QZ_ATTN_ABL;
 constexpr int kAttnMaxG = 8;     // query heads per kv head
+// s_v row padding (dwords): each thread stages its half row of v at s_v[position][half * H2/2 ...];
+// with an unpadded 64-dword row every lane of a write group lands on the same bank (32-way for
+// ds_write_b32, 8-way for b128); a 4-dword pad spreads 8 consecutive positions over all 32 banks.
+// (QZ_ATTN_VPAD=0: measurement build of the unpadded image, scripts/dev/build_attn_abl.sh)
+#ifndef QZ_ATTN_VPAD
+#define QZ_ATTN_VPAD 4
+#endif
+constexpr int kAttnVPad = QZ_ATTN_VPAD;
 constexpr int kAttnSpecL = 512;  // caches read before their mask arrives (speculatively) up to this length
 
 struct DecodeAttnArgs {
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   __shared__ uint32_t s_qh[H2];                        // rotated q, raw (the layout of s_kn)
   __shared__ float s_sc[2][kAttnChunk];                // half-row partial scores
   __shared__ float s_p[kAttnChunk];                    // probabilities (0: masked / past L)
-  __shared__ uint32_t s_v[kAttnChunk][H2];             // raw v rows (zero where masked)
+  __shared__ uint32_t s_v[kAttnChunk][H2 + kAttnVPad];  // raw v rows (zero where masked), padded rows
   __shared__ uint32_t s_kn[H2], s_vn[H2];              // the new (rotated) k and v, raw
   __shared__ unsigned char s_ok[kAttnChunk];
   __shared__ float s_pv[4 * NSUB][D];                  // P V partials of the position slices

@@ -41,7 +41,7 @@ for r in (4, 2, 8):
         _lib.set_gemv_knob("QZ_PAIR_PS", ps)
         t = graph_time(lambda i: gemv_4bit_pair_silu(x, copies[i % NC], exact_codes=True))
         print(f"whole-row pair R={r} QZ_PAIR_PS={ps}: {t:.2f} us", flush=True)
-_lib.set_gemv_knob("QZ_PAIR_WK1", 0)
+_lib.set_gemv_knob("QZ_PAIR_WK1", 1)
 _lib.set_gemv_knob("QZ_PAIR_R", 0)
 _lib.set_gemv_knob("QZ_PAIR_PS", -1)
 # with the norm: the norm launch + the whole-row pair (default) against the norm fused into the

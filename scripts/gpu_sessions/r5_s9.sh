@@ -22,8 +22,6 @@ pmc() {  # name cmd... (one PMC pass, killed hard at 120 s)
   echo "== $name rc=$rc"; tail -1 "gpurun_out/$name.log" | cut -c1-200
   [ $rc -eq 0 ] || exit $rc
 }
-step r5o_attn_pad 200 python3 scripts/dev/attn_pad_ab.py
-step r5o_attn_tests 300 python3 -u -m pytest tests/test_gpu_decode_attention.py -x -q --timeout 120 --timeout-method thread
 step r5o_pair70 300 python3 scripts/dev/pair_split_times.py
 step r5o_census70 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r5o_census70 -o run --output-format csv -- python3 bench.py --model llama3-70b --no-prefill --no-cpu --no-roofline --steps 16 --warmup 4
 for n in 1 2 4 8; do

@@ -331,8 +331,8 @@ int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const v
  * qz_silu_mul.  norm_weight (nullable): x is first RMSNorm'd as qz_gemv_4bit_grouped_rmsnorm does.
  * Where the grouped geometry splits K over waves (K = 8192: Llama-3-70B) the pair keeps whole rows
  * per wave -- another fp32 summation order, within fp16 rounding of the grouped launch, not its
- * bits -- and declines a fused norm (QZ_ERR_SHAPE: run qz_rmsnorm, then this without the norm);
- * the QZ_PAIR_WK1 knob (qz_gemv_set_knob) = 2 fuses the norm there, 0 declines those geometries.
+ * bits; the QZ_PAIR_WK1 knob (qz_gemv_set_knob) = 1 declines a fused norm there (QZ_ERR_SHAPE: run
+ * qz_rmsnorm, then this without the norm), 0 declines those geometries.
  * F16/BF16, full K-steps (K % 2048 == 0); otherwise QZ_ERR_SHAPE and nothing launched. */
 int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
                            int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,

@@ -56,7 +56,7 @@ static Knobs read_knobs() {
   k.pair_r = (pr == 2 || pr == 3 || pr == 4 || pr == 6 || pr == 8) ? pr : 0;
   k.pair_wt = env_int("QZ_PAIR_WT", 1) != 0;
   k.pair_ps = env_int("QZ_PAIR_PS", -1);
-  k.pair_wk1 = env_int("QZ_PAIR_WK1", 1);
+  k.pair_wk1 = env_int("QZ_PAIR_WK1", 2);
   return k;
 }
 static Knobs g_knobs = read_knobs();   // at library load
@@ -427,9 +427,10 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
     // K split over waves in the grouped launch (the K = 8192 layers of Llama-3-70B; small pairs):
     // the pair keeps whole rows per wave -- the same products in another fp32 summation order
     // (faster: 28672 x 8192 gate/up 52-55 us against 57-59 for the grouped launch and 60-61 for a
-    // split-K pair, profiles/r5_pair_k8192_forms.txt).  Without the norm: with it (7168 workgroups
-    // each normalising 16 KiB of x) the pair took 70.8 us, so QZ_ERR_SHAPE and the caller runs the
-    // norm launch first (QZ_PAIR_WK1=2 fuses it anyway; 0 declines these geometries altogether)
+    // split-K pair, profiles/r5_pair_k8192_forms.txt), with the norm fused in persistent workgroups
+    // at 3 per CU (54.6 us against 55.7 for the norm launch + the pair, 58.2 on the 64 KiB table
+    // that fits once per CU: profiles/r5_pair70_norm_forms.txt).  QZ_PAIR_WK1=1: the norm as its own
+    // launch (QZ_ERR_SHAPE with a norm: the caller runs it first); 0: these geometries declined
     const int wk1 = gemv_knobs().pair_wk1;
     if (wk1 == 0 || (norm_weight && wk1 != 2)) return QZ_ERR_SHAPE;
     WK = 1;

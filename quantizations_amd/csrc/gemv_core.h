@@ -971,9 +971,9 @@ struct Knobs {
   int pair_wt;  // QZ_PAIR_WT=0: the persistent pair keeps the 16-copy exact table (default 1)
   int pair_ps;  // QZ_PAIR_PS: 0 = one workgroup per block, 1..8 = workgroups per CU, >= 16 = the grid; -1 = default
   int pair_wk1; // QZ_PAIR_WK1: where the grouped geometry splits K over waves (K = 8192), the pair launch
-                // 1 (default): keeps whole rows per wave, without a fused norm (with one: declines, the caller
-                // runs the norm launch first); 2: fuses the norm there too (slower: 70B 91.7 vs 95.9 tok/s,
-                // profiles/r5_pair_k8192_ab.txt); 0: declines (round 4: grouped launch + SiLU launch)
+                // 2 (default): keeps whole rows per wave, the norm fused (persistent, as many per CU as the
+                // LDS admits); 1: whole rows, a norm declined (the caller runs the norm launch first);
+                // 0: declines these geometries (round 4: grouped launch + SiLU launch)
 };
 // the knobs the library read at load (gemv.hip); qz_gemv_set_knob changes one explicitly
 Knobs &gemv_knobs();

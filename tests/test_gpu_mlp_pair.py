@@ -21,7 +21,7 @@ def knobs():
     from quantizations_amd import _lib
 
     yield _lib.set_gemv_knob
-    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0), ("QZ_PAIR_WK1", 1)):
+    for name, v in (("QZ_PAIR_PS", -1), ("QZ_PAIR_WT", 1), ("QZ_PAIR_R", 0), ("QZ_PAIR_WK1", 2)):
         _lib.set_gemv_knob(name, v)
 
 
@@ -147,9 +147,9 @@ def _rel_to_grouped(h, gate, up):
 def test_pair_silu_whole_rows_at_k8192(knobs, M, norm, bias, quant, dq):
     """K = 8192, where the grouped launch splits K over two waves: the pair keeps whole rows per wave
     -- the same products in another fp32 summation order, so within fp16 rounding of the grouped
-    launch + product.  With a norm, the C entry declines the fused prologue and core runs the norm
-    launch, then the pair: bit-identical to norm launch -> pair without norm.  QZ_PAIR_WK1=2 fuses the
-    norm (same bits as norm launch + pair), 0 declines (None, nothing launched)."""
+    launch + product.  With a norm it is fused (persistent workgroups): bit-identical to norm launch ->
+    pair without norm, which is what QZ_PAIR_WK1=1 runs (the C entry declines, core launches the
+    norm first); 0 declines (None, nothing launched)."""
     from quantizations_amd.core import LAST_FORM, gemv_4bit_grouped, gemv_4bit_pair_silu
     from quantizations_amd.layer_ops import rms_norm
 
@@ -161,15 +161,15 @@ def test_pair_silu_whole_rows_at_k8192(knobs, M, norm, bias, quant, dq):
     nrm = (nw, 1e-5) if norm else None
     h = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=nrm)
     assert h is not None
-    assert LAST_FORM["pair"] == ("norm launch + pair" if norm else "pair")
+    assert LAST_FORM["pair"] == ("pair (norm fused)" if norm else "pair")
     xn = rms_norm(x, nw, 1e-5) if norm else x
     gate, up = gemv_4bit_grouped(xn, items, exact_codes=True)
     assert _rel_to_grouped(h, gate, up) < 2e-3
     if norm:
         assert torch.equal(h, gemv_4bit_pair_silu(xn, items, exact_codes=True))
-        knobs("QZ_PAIR_WK1", 2)
+        knobs("QZ_PAIR_WK1", 1)
         h2 = gemv_4bit_pair_silu(x, items, exact_codes=True, norm=nrm)
-        assert LAST_FORM["pair"] == "pair (norm fused)" and torch.equal(h2, h)
+        assert LAST_FORM["pair"] == "norm launch + pair" and torch.equal(h2, h)
     knobs("QZ_PAIR_WK1", 0)
     assert gemv_4bit_pair_silu(xn, items, exact_codes=True) is None
 

@@ -1007,7 +1007,7 @@ static inline bool two_steps(int K, int WK, bool fs) { return fs && WK == 1 && K
 
 // Geometry (WK = waves along K, R = rows per wave) for the byte-table decode,
 // from the measured shape sweep in DESIGN.md section 4.1:
-//  * >= 64 Mi weights (gate/up groups, 8192x28672, ...): R=4 -- more bytes in
+//  * > 64 Mi weights (gate/up groups, 8192x28672, ...): R=4 -- more bytes in
 //    flight per wave and fewer x/scale loads per weight byte;
 //  * smaller: R=2;
 //  * WK=1 (a wave owns whole rows: no cross-wave reduction), then R halves /
@@ -1018,7 +1018,9 @@ static inline bool two_steps(int K, int WK, bool fs) { return fs && WK == 1 && K
 static void choose_geometry(int M, int K, int dtype, int *R, int *WK) {
   const int nsteps = ((K >> 1) + 1023) >> 10;
   const bool f32 = dtype == QZ_DT_F32;
-  *R = (f32 || (long long)M * K >= (1LL << 26)) ? 4 : 2;
+  // (exactly 64 Mi weights -- the Llama-3-70B o_proj, 8192 x 8192 -- takes R = 2 with whole rows:
+  //  10.37 vs 10.85 us at R = 4, WK = 2, profiles/r5_pair_k8192_forms.txt geom8k)
+  *R = (f32 || (long long)M * K > (1LL << 26)) ? 4 : 2;
   *WK = 1;
   // * 4 K-steps per row (K = 8192, the Llama-3-70B q/k/v, o and gate/up) at R=4: two waves per
   //   row, two steps each (profiles/r2_gemv_wk70.txt: 10240x8192 14.0 -> 11.3 us, 8192^2 11.0 ->

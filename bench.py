@@ -198,7 +198,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = False):
+                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -231,7 +231,8 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
                                      residual=residual, mlp_pair=mlp_pair,
-                                     mlp_chain=mlp_chain)  # one launch each
+                                     mlp_chain=mlp_chain,
+                                     qkv_attention=qkv_attention)  # one launch each
     if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -1140,6 +1141,9 @@ def main():
                     help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
                          "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
                          "barriers cost more than launch boundaries, DESIGN.md section 12)")
+    ap.add_argument("--no-qkv-attention", action="store_true",
+                    help="q/k/v projections and the decode attention as two launches (default: one, the attention "
+                         "of each head in the q/k/v launch's tail, csrc/qkv_attn.hip)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -1246,7 +1250,8 @@ def main():
                                                      attention=not args.no_attention,
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
-                                                     mlp_chain=args.mlp_chain)
+                                                     mlp_chain=args.mlp_chain,
+                                                     qkv_attention=not args.no_qkv_attention)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1358,6 +1363,9 @@ def main():
         line["config"]["mlp_chain_launch"] = bool(args.mlp_chain and not args.no_residual and not args.no_attention
                                                   and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
                                                   and not sharded)
+        line["config"]["qkv_attention_launch"] = bool(not args.no_qkv_attention and not args.no_attention
+                                                      and not args.no_fuse and layer_ops in ("all", "all+decoder")
+                                                      and not sharded)
         line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"
         line["config"]["knobs"] = _safe(effective_knobs)
         if exchange is not None:

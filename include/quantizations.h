@@ -358,6 +358,23 @@ int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz
                  unsigned *state, void *stream);
 int qz_mlp_chain_state_words(void);
 
+/* A decode token's q/k/v projections AND its attention in ONE launch (round 5, not in the reference;
+ * csrc/qkv_attn.hip): qz_gemv_4bit_grouped(_rmsnorm) over segs[0..2] = q_proj, k_proj, v_proj
+ * (M = Hq*D, Hkv*D, Hkv*D; their `y` receive q, k, v as before), then qz_decode_attention's rotary,
+ * cache update, pos += 1 and masked GQA attention for one sequence (B = 1) over a static cache of
+ * L <= 128 positions, out = [Hq*D].  Each query head's attention runs in the q/k/v launch, by the
+ * last workgroup that stored the head's rows.  Bit-identical to the two launches.  `state`:
+ * qz_qkv_attention_state_words(Hq, Hkv) int32 words, zeroed ONCE and then owned by the calls (one
+ * per stream); word (Hq + Hkv + 1) * 32 becomes nonzero if a wait ever gave up.  Shapes the fused
+ * launch does not take (L > 128, geometries that split K over waves or put two heads in a
+ * workgroup, fp32, unaligned outputs): QZ_ERR_SHAPE, nothing launched -- run the two launches. */
+int qz_gemv_4bit_qkv_attention(const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
+                               int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,
+                               int Hq, int Hkv, int D, int L, const void *cos, const void *sin, void *k_cache,
+                               void *v_cache, const void *mask, long long mask_j, long long *pos, void *out,
+                               float scale, unsigned *state, void *stream);
+int qz_qkv_attention_state_words(int Hq, int Hkv);
+
 /* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
  * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1: environment variables read ONCE when the library is loaded) and the
  * device's CU count, as a JSON object written to buf (NUL-terminated when n > the length).

@@ -250,8 +250,6 @@ extern "C" int qz_gemv_4bit_residual(int M, int K, const void *x, int dtype, con
 
 // nw != nullptr: x is first RMSNorm'd with weight nw / epsilon eps, bit-identically to qz_rmsnorm
 // (the pre-norm of q/k/v and gate/up fused into their grouped launch)
-constexpr int kNormMaxBlocks = 4096;
-constexpr size_t kLdsPerCU = 160 * 1024;   // gfx950: LDS per compute unit
 static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
                              int blocksize, int blocksize2, const float *lut, const void *nw, float eps, void *stream) {
   if (nseg < 1 || nseg > QZ_GEMV_MAX_SEGMENTS || !segs) return QZ_ERR_ARG;

@@ -6,6 +6,4 @@ for a in 0 1 2 4 8 16 32; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-rdc -shared \
     -DQZ_ATTN_ABL=$a -o ../../scripts/dev/attn_abl/libattn_$a.so layer_ops.hip &
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-rdc -shared \
-  -DQZ_ATTN_ABL=0 -DQZ_ATTN_VPAD=0 -o ../../scripts/dev/attn_abl/libattn_0_nopad.so layer_ops.hip &
 wait

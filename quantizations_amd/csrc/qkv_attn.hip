@@ -80,6 +80,11 @@ template <int DT, int D> struct QkvAttnTail {
       if (n >= kQaSpinLimit) qa_store(cnt + (Hq + Hkv + 1) * kQaLine, 1u);
     }
     __syncthreads();
+    // an agent-scope acquire before the head's loads: with several workgroups per CU and 128-B lines
+    // of q / k / v written piecewise by workgroups on other XCDs, an sc1 load alone may be served a
+    // stale line (MI355X_MICROARCH.md's measured sc1 hand-offs without an acquire hold for one
+    // workgroup per CU only)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const AttnLds<D> S{reinterpret_cast<uint32_t *>(big), small};
     const long long p = decode_attn_head<DT, D, true>(qa->a, 0, hq, 0, S);
     __syncthreads();

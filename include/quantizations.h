@@ -363,7 +363,9 @@ int qz_mlp_chain_state_words(void);
  * (M = Hq*D, Hkv*D, Hkv*D; their `y` receive q, k, v as before), then qz_decode_attention's rotary,
  * cache update, pos += 1 and masked GQA attention for one sequence (B = 1) over a static cache of
  * L <= 128 positions, out = [Hq*D].  Each query head's attention runs in the q/k/v launch, by the
- * last workgroup that stored the head's rows.  Bit-identical to the two launches.  `state`:
+ * last workgroup that stored the head's rows; the segments' `y` (the q, k, v hand-off) must be
+ * UNCACHED device memory (qz_exchange_alloc), or readers may see the previous call's rows.
+ * Bit-identical to the two launches.  `state`:
  * qz_qkv_attention_state_words(Hq, Hkv) int32 words, zeroed ONCE and then owned by the calls (one
  * per stream); word (Hq + Hkv + 1) * 32 becomes nonzero if a wait ever gave up.  Shapes the fused
  * launch does not take (L > 128, geometries that split K over waves or put two heads in a

@@ -501,6 +501,27 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     return h
 
 
+_QKV_SCRATCH = {}
+
+
+def _qkv_scratch(device, nbytes: int) -> int:
+    """Uncached device memory (qz_exchange_alloc: hipDeviceMallocUncached) for the q / k / v rows the
+    fused q/k/v + attention launch hands from its GEMV workgroups to its attention workgroups: with
+    several workgroups per CU, cached lines of the previous call's rows at the same addresses were
+    served to the readers even behind write-through stores and an agent-scope acquire
+    (scripts/dev/qkv_attn_debug4.py); uncached memory has no lines to go stale.  One buffer per
+    device and size, allocated outside any graph capture (the decode warms up eagerly first)."""
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    key = (dev, int(nbytes))
+    p = _QKV_SCRATCH.get(key)
+    if p is None:
+        vp = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(lib.qz_exchange_alloc(int(nbytes), ctypes.byref(vp)), "qz_exchange_alloc")
+        p = _QKV_SCRATCH[key] = vp.value
+    return p
+
+
 def qkv_attention_state(num_heads: int, num_kv_heads: int, device) -> Tensor:
     """Counter words of qz_gemv_4bit_qkv_attention (int32, zeroed once; one per stream)."""
     return torch.zeros(int(lib.qz_qkv_attention_state_words(int(num_heads), int(num_kv_heads))), dtype=torch.int32,
@@ -547,13 +568,15 @@ def gemv_4bit_qkv_attention(x: Tensor, items, norm, cos: Tensor, sin: Tensor, ke
         return None
     x = x.contiguous()
     segs = (_lib.GemvSegment * 3)()
+    rows = [it[1].shape[0] for it in items]
+    base = _qkv_scratch(x.device, 2 * sum(rows))   # q, k, v back to back, 16-bit
+    offs = [0, 2 * rows[0], 2 * (rows[0] + rows[1])]
     for i, it in enumerate(items):
         B, st, bias = it[0], it[1], it[2] if len(it) > 2 else None
         if bias is not None and bias.dtype != x.dtype:
             bias = bias.to(x.dtype)
-        y = torch.empty((1, 1, st.shape[0]), dtype=x.dtype, device=x.device)
         am, qam, am2, code2, off, _ = st.scale_args()
-        segs[i] = _lib.GemvSegment(st.shape[0], ptr(B), am, qam, am2, code2, off, 0, ptr(bias), ptr(y))
+        segs[i] = _lib.GemvSegment(st.shape[0], ptr(B), am, qam, am2, code2, off, 0, ptr(bias), base + offs[i])
     out = torch.empty((1, 1, num_heads * D), dtype=x.dtype, device=x.device)
     bs2 = int(s0.state2.blocksize) if s0.nested else 0
     rc = lib.qz_gemv_4bit_qkv_attention(ctypes.cast(segs, ctypes.c_void_p), K, ptr(x), dtype_code(x.dtype),

@@ -9,6 +9,13 @@
 // agent-scope atomics; the LAST workgroup to store a query head's rows runs that head's attention
 // (attn_core.h, bit-identical arithmetic, q/k/v read at agent scope) in the LDS its decode used.
 //
+// Visibility: the q / k / v rows live in UNCACHED device memory (the caller's buffers, e.g.
+// core._qkv_scratch: hipDeviceMallocUncached).  In cached (hipMalloc) memory the readers were served
+// lines of the PREVIOUS call's rows at the same addresses -- behind write-through stores, agent-scope
+// loads and even an agent-scope acquire -- with three workgroups per CU (the guide's measured sc1
+// hand-offs hold for one per CU); uncached lines cannot go stale.  The stores stay write-through and
+// the loads agent-scope, so the protocol does not depend on the memory type beyond that.
+//
 // Ordering and progress: the grid is laid out k, v, q (segments in that order), so every k and v
 // workgroup is dispatched before any q workgroup.  A query head's attention needs its kv head's k
 // and v rows too: the q workgroup that completes the head waits (bounded, s_sleep) for the kv
@@ -80,11 +87,6 @@ template <int DT, int D> struct QkvAttnTail {
       if (n >= kQaSpinLimit) qa_store(cnt + (Hq + Hkv + 1) * kQaLine, 1u);
     }
     __syncthreads();
-    // an agent-scope acquire before the head's loads: with several workgroups per CU and 128-B lines
-    // of q / k / v written piecewise by workgroups on other XCDs, an sc1 load alone may be served a
-    // stale line (MI355X_MICROARCH.md's measured sc1 hand-offs without an acquire hold for one
-    // workgroup per CU only)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const AttnLds<D> S{reinterpret_cast<uint32_t *>(big), small};
     const long long p = decode_attn_head<DT, D, true>(qa->a, 0, hq, 0, S);
     __syncthreads();

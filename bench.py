@@ -198,7 +198,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = True):
+                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -1141,9 +1141,10 @@ def main():
                     help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
                          "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
                          "barriers cost more than launch boundaries, DESIGN.md section 12)")
-    ap.add_argument("--no-qkv-attention", action="store_true",
-                    help="q/k/v projections and the decode attention as two launches (default: one, the attention "
-                         "of each head in the q/k/v launch's tail, csrc/qkv_attn.hip)")
+    ap.add_argument("--qkv-attention", action="store_true",
+                    help="q/k/v projections and the decode attention as ONE launch (each head's attention in the "
+                         "q/k/v launch's tail, csrc/qkv_attn.hip; measured slower than the default two launches, "
+                         "DESIGN.md section 12)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -1251,7 +1252,7 @@ def main():
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
                                                      mlp_chain=args.mlp_chain,
-                                                     qkv_attention=not args.no_qkv_attention)
+                                                     qkv_attention=args.qkv_attention)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1363,7 +1364,7 @@ def main():
         line["config"]["mlp_chain_launch"] = bool(args.mlp_chain and not args.no_residual and not args.no_attention
                                                   and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
                                                   and not sharded)
-        line["config"]["qkv_attention_launch"] = bool(not args.no_qkv_attention and not args.no_attention
+        line["config"]["qkv_attention_launch"] = bool(args.qkv_attention and not args.no_attention
                                                       and not args.no_fuse and layer_ops in ("all", "all+decoder")
                                                       and not sharded)
         line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"

@@ -461,7 +461,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
                    decoder: bool = False, attention: bool = True, residual: bool = True,
-                   mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = True) -> int:
+                   mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -481,8 +481,10 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     post-attention norm, MLP and second residual as ONE persistent launch (_mlp_chain) where the
     layer qualifies (after fuse_prenorm): bit-identical, but measured slower than the three launches
     (each in-kernel grid barrier costs 6-7 us against a ~1.5 us launch boundary).
-    `qkv_attention` (with `attention`) lets a decode token's q/k/v projections and attention run as
-    ONE launch where the projections form a plain Linear4bit decode group (_qkv_attention)."""
+    `qkv_attention` (opt-in, with `attention`) lets a decode token's q/k/v projections and attention
+    run as ONE launch where the projections form a plain Linear4bit decode group (_qkv_attention):
+    bit-identical, but measured slower than the two launches (Llama-3-8B decode 577 vs 590 tok/s on
+    one box)."""
     import sys
 
     n = 0

@@ -143,7 +143,7 @@ def _model(dtype, layers=2):
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_llama_decode_with_qkv_attention_equals_two_launches(dtype):
-    """bench.py's decode loop (HIP graph) with the fused q/k/v + attention launch in every layer,
+    """bench.py's decode loop (HIP graph) with the fused q/k/v + attention launch in every layer (opt-in),
     against the same model with it switched off: identical greedy tokens; the fused launch ran."""
     import bench
     import quantizations_amd.integration as integ

@@ -534,11 +534,11 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
             "achieved": round(nbytes / (us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "other_codes_launch_us": round(other_us, 3), "plain_grouped_launch_us": round(plain_us, 3),
-            "traffic": _pmc_traffic("r4_pair_wide_pmc.json") if (prenorm and pair)
+            "traffic": _pmc_traffic("r5_pair_wide_pmc.json") if (prenorm and pair)
             else _pmc_traffic("r3_gateup_pmc.json"),
-            "profile": ("profiles/r4_pair_wide_pmc.json (rocprofv3 FETCH/WRITE passes of THIS launch: the "
+            "profile": ("profiles/r5_pair_wide_pmc.json (rocprofv3 FETCH/WRITE passes of THIS launch: the "
                         "persistent pair with the norm and SiLU, exact codes on the 256-B-entry table; SQ counters "
-                        "profiles/r4_pair_wide_sq_counters.txt, kernel trace r4_pair_wide_trace_stats.txt)"
+                        "profiles/r5_pair_wide_sq_counters.txt, kernel trace r5_pair_wide_trace_stats.txt)"
                         if (prenorm and pair) else
                         "profiles/r3_gateup_pmc.json (rocprofv3 kernel trace + FETCH/WRITE passes of the grouped "
                         "launch without the norm)")}

@@ -294,10 +294,6 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   // QZ_GROUPED_NORM_R (knob): rows per wave of the fused pre-norm launch where the geometry keeps
   // whole rows per wave (WK = 1: the same per-row sums)
   if (nw && gemv_knobs().norm_r && WK == 1) R = gemv_knobs().norm_r;
-  // where K is split over waves (K = 8192: the Llama-3-70B q/k/v) the norm launch + the plain grouped
-  // launch beat the fused prologue, repeated by 1280 small workgroups (16.41 vs 17.23 us,
-  // profiles/r5_qkv70_forms.txt): the caller runs the two launches
-  if (nw && WK != 1) return QZ_ERR_SHAPE;
   const int rows_per_block = R * (4 / WK);
   int blocks = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -312,6 +308,11 @@ static int gemv_grouped_impl(int nseg, const qz_gemv_segment *segs, int K, const
   // Llama-3-70B gate/up, 7168 workgroups, 74.6 us fused vs 58.6 us for the two launches;
   // profiles/r3_prenorm_launch_times.txt)
   if (nw && blocks > kNormMaxBlocks) return QZ_ERR_SHAPE;
+  // where K is split over waves and the prologue is large (the Llama-3-70B q/k/v: 1280 workgroups
+  // each normalising 8192 values) the norm launch + the plain grouped launch beat the fused prologue
+  // (16.41 vs 17.23 us, profiles/r5_qkv70_forms.txt): the caller runs the two launches.  A row
+  // shard's q/k/v (Llama-3-8B at N = 8: 384 workgroups x 4096) keeps it fused (round 4's form).
+  if (nw && WK != 1 && (long long)blocks * K > kNormSplitMaxValues) return QZ_ERR_SHAPE;
   bool all_fs = true;
   for (int i = 0; i < nseg; ++i) all_fs = all_fs && full_steps(K, blocksize, blocksize2, dq, segs[i].block_base);
   hipStream_t s = (hipStream_t)stream;

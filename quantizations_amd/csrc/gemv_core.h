@@ -992,6 +992,8 @@ struct Knobs {
                 // 0: declines these geometries (round 4: grouped launch + SiLU launch)
 };
 constexpr int kNormMaxBlocks = 4096;
+// fused norm prologue at K-split geometries: at most this many normalised values over all workgroups
+constexpr long long kNormSplitMaxValues = 1LL << 23;
 constexpr size_t kLdsPerCU = 160 * 1024;   // gfx950: LDS per compute unit
 // the knobs the library read at load (gemv.hip); qz_gemv_set_knob changes one explicitly
 Knobs &gemv_knobs();

@@ -52,6 +52,27 @@ def test_grouped_gemv_rmsnorm_bit_identical_to_two_launches(dtype, exact, Ms, K)
         assert torch.equal(a, b), f"segment {i}: {(a.float() - b.float()).abs().max().item()}"
 
 
+@pytest.mark.parametrize("Ms,K,form", [((512, 128, 128), 4096, "grouped (norm fused)"),     # 8B q/k/v, 8-way shard
+                                       ((1024, 128, 128), 8192, "grouped (norm fused)"),    # 70B q/k/v, 8-way shard
+                                       ((8192, 1024, 1024), 8192, "norm launch + grouped")])  # 70B q/k/v whole
+def test_grouped_rmsnorm_at_k_split_geometries(Ms, K, form):
+    """Where K is split over waves: a row shard's q/k/v (few workgroups) keeps the norm fused, the
+    whole Llama-3-70B q/k/v (1280 workgroups x 8192 values) takes the norm launch; bit-identical either way."""
+    from quantizations_amd.core import LAST_FORM, gemv_4bit_grouped
+    from quantizations_amd.layer_ops import rms_norm
+
+    items = _items(Ms, K, torch.float16, seed=K + Ms[0], bias_seg=-1)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.randn(1, 1, K, device=DEV, generator=g) * 3).half()
+    w = (1.0 + 0.1 * torch.randn(K, device=DEV, generator=g)).half()
+    ref = gemv_4bit_grouped(rms_norm(x, w, 1e-5), items, exact_codes=True)
+    got = gemv_4bit_grouped(x, items, exact_codes=True, norm=(w, 1e-5))
+    torch.cuda.synchronize()
+    assert LAST_FORM["grouped"] == form
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_grouped_gemv_rmsnorm_fp4_without_double_quant(dtype):
     """Config #3's format (FP4, fp32 absmax): the other scale path of the fused launch."""

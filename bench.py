@@ -115,7 +115,7 @@ def decode_bench(model, cfg, steps: int, warmup: int, prompt_len: int, world: in
     return dt, torch.cat(toks, dim=1)
 
 
-TWO_STAGE_ARGMAX = True   # --torch-argmax: the decode step's greedy pick as one torch.argmax (A/B)
+GREEDY = "kernel"   # --greedy: the decode step's greedy pick + feedback ("kernel": layer_ops.greedy_step)
 
 
 def greedy_token(logits: torch.Tensor) -> torch.Tensor:
@@ -159,7 +159,11 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
     def step():
         lo = model(input_ids=tok, past_key_values=cache, cache_position=pos, position_ids=pos_ids,
                    use_cache=True).logits
-        nxt = greedy_token(lo[:, -1:]) if TWO_STAGE_ARGMAX else lo[:, -1:].argmax(-1)
+        if GREEDY == "kernel" and lo.is_cuda:
+            from quantizations_amd.layer_ops import greedy_step
+            greedy_step(lo[:, -1], hist, pos, tok)   # argmax + the three feedback writes, one launch
+            return
+        nxt = greedy_token(lo[:, -1:]) if GREEDY == "two-stage" else lo[:, -1:].argmax(-1)
         hist.index_copy_(1, pos, nxt.view(batch, 1))
         tok.copy_(nxt)
         pos.add_(1)
@@ -198,7 +202,8 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False):
+                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False,
+                         glue: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -236,6 +241,9 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
     if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
+    if glue and layer_ops != "none":
+        from quantizations_amd.integration import fuse_decode_glue
+        n_layer_ops += fuse_decode_glue(model)   # the step's causal mask and rotary cos/sin: one launch each
     return n_groups, n_layer_ops
 
 
@@ -1132,6 +1140,9 @@ def main():
     ap.add_argument("--no-attention", action="store_true",
                     help="keep transformers' rotary + StaticCache update + sdpa (14 launches per layer) instead of "
                          "the one-launch layer_ops.decode_attention")
+    ap.add_argument("--greedy", choices=("kernel", "two-stage", "torch"), default="kernel",
+                    help="the decode step's greedy pick: one launch with the token feedback (layer_ops.greedy_step), "
+                         "greedy_token's two stages, or torch.argmax (the last two + index_copy/copy/add)")
     ap.add_argument("--torch-argmax", action="store_true",
                     help="the decode step's greedy pick as torch's one-pass argmax (default: greedy_token's two "
                          "stages, the same index)")
@@ -1141,6 +1152,9 @@ def main():
                     help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
                          "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
                          "barriers cost more than launch boundaries, DESIGN.md section 12)")
+    ap.add_argument("--no-glue", action="store_true",
+                    help="keep transformers' own causal-mask and rotary code in the decode step (default: one "
+                         "launch each, integration.fuse_decode_glue; same values)")
     ap.add_argument("--qkv-attention", action="store_true",
                     help="q/k/v projections and the decode attention as ONE launch (each head's attention in the "
                          "q/k/v launch's tail, csrc/qkv_attn.hip; measured slower than the default two launches, "
@@ -1236,8 +1250,8 @@ def main():
     layer_ops = "none" if args.no_layer_ops else args.layer_ops
 
     compute_dtype = torch.float32 if args.compute_dtype == "fp32" else torch.float16
-    global TWO_STAGE_ARGMAX
-    TWO_STAGE_ARGMAX = not args.torch_argmax
+    global GREEDY
+    GREEDY = "torch" if args.torch_argmax else args.greedy
 
     def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int, cdt: torch.dtype = compute_dtype):
         t_build = time.perf_counter()
@@ -1252,7 +1266,8 @@ def main():
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
                                                      mlp_chain=args.mlp_chain,
-                                                     qkv_attention=args.qkv_attention)
+                                                     qkv_attention=args.qkv_attention,
+                                                     glue=not args.no_glue)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1367,7 +1382,9 @@ def main():
         line["config"]["qkv_attention_launch"] = bool(args.qkv_attention and not args.no_attention
                                                       and not args.no_fuse and layer_ops in ("all", "all+decoder")
                                                       and not sharded)
-        line["config"]["greedy_argmax"] = "torch.argmax" if args.torch_argmax else "two-stage (greedy_token)"
+        line["config"]["decode_glue_launches"] = bool(not args.no_glue and layer_ops != "none")
+        line["config"]["greedy_argmax"] = {"kernel": "one launch with the feedback (layer_ops.greedy_step)",
+                                           "two-stage": "two-stage (greedy_token)", "torch": "torch.argmax"}[GREEDY]
         line["config"]["knobs"] = _safe(effective_knobs)
         if exchange is not None:
             line["config"]["exchange"] = exchange

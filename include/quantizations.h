@@ -324,6 +324,27 @@ int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const v
                         long long mask_b, long long mask_j, long long *pos, unsigned int *arrive, void *out,
                         long long out_row, float *work, float scale, void *stream);
 
+/* Decode-step glue of the host model (transformers' LlamaModel.forward), one launch each in place
+ * of the small torch kernels it issues per step.  Not part of the Linear4bit path; the
+ * integration (integration.fuse_decode_glue) takes them only where they give the same values.
+ * qz_decode_mask: masking_utils.create_causal_mask for one new token against a static cache
+ *   (sdpa, causal, no padding mask, kv_offset 0): mask[b*L + j] = (j <= *q_offset), bool bytes,
+ *   q_offset = StaticLayer.cumulative_length (device int64, read in-kernel).
+ * qz_rope_table: LlamaRotaryEmbedding.forward for positions pos[b*pos_b + s*pos_s]: cos/sin
+ *   [B, S, D] contiguous copied from the [T, D] tables that module computed for positions 0..T-1;
+ *   a position outside [0, T) is computed from inv_freq [D/2] (fp32 product, cosf/sinf, * scale,
+ *   rounded to dtype).  D even; F16/BF16/F32. */
+/* qz_greedy_step: the greedy pick and its feedback, one workgroup: for b < B,
+ *   next = argmax_v logits[b*row + v] (v < V; torch.argmax's order: NaN above every number,
+ *   the first index among equals), hist[b*hist_row + *pos] = next, tok[b] = next; then *pos += 1.
+ *   int64 hist/pos/tok on the device (graph-capturable); F16/BF16/F32 logits. */
+int qz_greedy_step(const void *logits, int dtype, int B, long long V, long long row, long long *hist,
+                   long long hist_row, long long hist_len, long long *pos, long long *tok, void *stream);
+int qz_decode_mask(const long long *q_offset, int B, int L, void *mask, void *stream);
+int qz_rope_table(int dtype, int B, int S, int D, const long long *pos, long long pos_b, long long pos_s,
+                  const void *cos_table, const void *sin_table, long long T, const float *inv_freq, float scale,
+                  void *cos, void *sin, void *stream);
+
 /* LlamaMLP's act_fn(gate_proj(x)) * up_proj(x) for hidden_act "silu" (modeling_llama.py:175) as
  * ONE launch: segs[0] = gate_proj, segs[1] = up_proj (equal M; their `y` are ignored), both
  * GEMVs as qz_gemv_4bit_grouped computes them, then h[r] = round(round(g / (1 + exp(-g))) * u)

@@ -79,6 +79,9 @@ SIGNATURES = {
     "qz_rmsnorm": [_p, _i, _ll, _i, _ll, _p, _f, _p, _ll, _p],
     "qz_rope_qk": [_i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p],
     "qz_silu_mul": [_p, _p, _i, _ll, _p, _p],
+    "qz_decode_mask": [_p, _i, _i, _p, _p],
+    "qz_greedy_step": [_p, _i, _i, _ll, _ll, _p, _ll, _ll, _p, _p, _p],
+    "qz_rope_table": [_i, _i, _i, _i, _p, _ll, _ll, _p, _p, _ll, _p, _f, _p, _p, _p],
     "qz_add_rmsnorm": [_p, _p, _i, _ll, _i, _ll, _p, _f, _p, _p, _ll, _p],
     "qz_bench_read_floor": [_p, _ll, _p, _p],
     "qz_bench_empty": [_p, _p],

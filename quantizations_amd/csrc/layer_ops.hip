@@ -305,6 +305,127 @@ int rmsnorm_entry(const void *x, const void *r, int dtype, long long rows, int K
   return (int)hipGetLastError();
 }
 
+// ---- decode-step glue of the host model (one launch each instead of the 7-9 small torch kernels
+// transformers' LlamaModel.forward issues per step; the Linear4bit layers are not touched) ----
+// causal mask of one new token per sequence against a static cache: masking_utils.sdpa_mask with
+// causal_mask_function and kv_offset 0 -- kv position j is visible iff j <= q_offset, the cache's
+// cumulative length before this token (a device int64, read in-kernel: graph-capturable)
+__global__ __launch_bounds__(256) void k_decode_mask(const long long *q_off, long long n, int L,
+                                                      unsigned char *mask) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  mask[i] = (long long)(i % L) <= q_off[0] ? 1 : 0;
+}
+
+// rotary cos/sin of the step's positions, looked up in [T, D] tables the model's own rotary module
+// computed for positions 0..T-1 (the same values, bit for bit); a position outside the table is
+// computed here from inv_freq (fp32 product, cosf/sinf, * scale, rounded to the dtype)
+struct RopeTableArgs {
+  const long long *pos;
+  long long pb, ps;                 // position_ids strides (batch, sequence)
+  const void *cos_t, *sin_t;        // [T, D]
+  const float *inv_freq;            // [D / 2]
+  void *cos, *sin;                  // [B, S, D], contiguous
+  long long n, T;
+  int S, D;
+  float scale;
+};
+template <int DT> __global__ __launch_bounds__(256) void k_rope_table(RopeTableArgs a) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const long long bs = i / a.D;
+  const int d = (int)(i - bs * a.D);
+  const long long b = bs / a.S, sq = bs - b * a.S;
+  const long long p = a.pos[b * a.pb + sq * a.ps];
+  if (p >= 0 && p < a.T) {
+    if constexpr (DT == QZ_DT_F32) {
+      reinterpret_cast<float *>(a.cos)[i] = reinterpret_cast<const float *>(a.cos_t)[p * a.D + d];
+      reinterpret_cast<float *>(a.sin)[i] = reinterpret_cast<const float *>(a.sin_t)[p * a.D + d];
+    } else {
+      reinterpret_cast<uint16_t *>(a.cos)[i] = reinterpret_cast<const uint16_t *>(a.cos_t)[p * a.D + d];
+      reinterpret_cast<uint16_t *>(a.sin)[i] = reinterpret_cast<const uint16_t *>(a.sin_t)[p * a.D + d];
+    }
+    return;
+  }
+  const float f = __fmul_rn(a.inv_freq[d % (a.D / 2)], (float)p);
+  store_f32<DT>(a.cos, i, __fmul_rn(cosf(f), a.scale));
+  store_f32<DT>(a.sin, i, __fmul_rn(sinf(f), a.scale));
+}
+
+// greedy pick + feedback of a decode step (bench.py's loop: next = argmax(logits[b]);
+// hist[b, *pos] = next; tok[b] = next; *pos += 1) in ONE workgroup: torch.argmax's order -- the
+// largest value, NaN above every number, the first index among equals
+constexpr int kGreedyThreads = 1024;
+__device__ __forceinline__ bool greedy_better(float v, long long i, float w, long long j) {
+  const bool vn = v != v, wn = w != w;
+  if (vn || wn) return vn && (!wn || i < j);
+  return v > w || (v == w && i < j);
+}
+template <int DT>
+__global__ __launch_bounds__(kGreedyThreads) void k_greedy_step(const void *logits, long long row, int B, long long V,
+                                                                long long *hist, long long hist_row, long long *pos,
+                                                                long long *tok, bool vec) {
+  __shared__ float s_v[kGreedyThreads / 64];
+  __shared__ long long s_i[kGreedyThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long p = *pos;
+  for (int b = 0; b < B; ++b) {
+    const void *lr = reinterpret_cast<const unsigned char *>(logits) + (size_t)b * row * (DT == QZ_DT_F32 ? 4 : 2);
+    float best = -__builtin_inff();
+    long long bi = V;   // no element yet
+    constexpr int E = DT == QZ_DT_F32 ? 4 : 8;   // elements per 16-B vector
+    if (vec) {
+      // 16-B loads, all of a thread's (up to 16: 128256 fp16 logits) in flight at once; a thread
+      // visits its elements in increasing index order, so a later equal value never replaces
+      typedef uint32_t w4_t __attribute__((ext_vector_type(4)));
+      const w4_t *vr = reinterpret_cast<const w4_t *>(lr);
+      const long long nv = V / E;
+      constexpr int U = 16;
+      for (long long q0 = tid; q0 < nv; q0 += (long long)U * kGreedyThreads) {
+        w4_t r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long q = q0 + (long long)u * kGreedyThreads;
+          r[u] = q < nv ? vr[q] : w4_t{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long long q = q0 + (long long)u * kGreedyThreads;
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const uint32_t w = r[u][DT == QZ_DT_F32 ? e : e >> 1];
+            float v;
+            if constexpr (DT == QZ_DT_F32) v = __uint_as_float(w);
+            else if constexpr (DT == QZ_DT_F16) v = __half2float(__ushort_as_half((unsigned short)((e & 1) ? w >> 16 : w & 0xFFFFu)));
+            else v = __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
+            if (q < nv && (v > best || (v != v && best == best) || bi == V)) { best = v; bi = q * E + e; }
+          }
+        }
+      }
+    } else {
+      for (long long i = tid; i < V; i += kGreedyThreads) {
+        const float v = load_f32<DT>(lr, i);
+        if (bi == V || greedy_better(v, i, best, bi)) { best = v; bi = i; }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float w = __shfl_xor(best, o);
+      const long long j = __shfl_xor(bi, o);
+      if (j != V && (bi == V || greedy_better(w, j, best, bi))) { best = w; bi = j; }
+    }
+    if (lane == 0) { s_v[wave] = best; s_i[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < kGreedyThreads / 64; ++w)
+        if (s_i[w] != V && (bi == V || greedy_better(s_v[w], s_i[w], best, bi))) { best = s_v[w]; bi = s_i[w]; }
+      hist[(size_t)b * hist_row + p] = bi;
+      tok[b] = bi;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *pos = p + 1;
+}
+
 }  // namespace
 }  // namespace qz
 
@@ -410,6 +531,58 @@ extern "C" int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int
   switch (dtype) {
     case QZ_DT_F16: D == 64 ? launch_decode_attn<QZ_DT_F16, 64>(a, B, s) : launch_decode_attn<QZ_DT_F16, 128>(a, B, s); break;
     case QZ_DT_BF16: D == 64 ? launch_decode_attn<QZ_DT_BF16, 64>(a, B, s) : launch_decode_attn<QZ_DT_BF16, 128>(a, B, s); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_decode_mask(const long long *q_offset, int B, int L, void *mask, void *stream) {
+  if (B < 0 || L < 0) return QZ_ERR_ARG;
+  if (B == 0 || L == 0) return 0;
+  if (!q_offset || !mask) return QZ_ERR_ARG;
+  const long long n = (long long)B * L, blocks = (n + 255) / 256;
+  if (blocks > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  hipLaunchKernelGGL(k_decode_mask, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, q_offset, n, L,
+                     reinterpret_cast<unsigned char *>(mask));
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_rope_table(int dtype, int B, int S, int D, const long long *pos, long long pos_b, long long pos_s,
+                             const void *cos_table, const void *sin_table, long long T, const float *inv_freq,
+                             float scale, void *cos, void *sin, void *stream) {
+  if (B < 0 || S < 0 || D < 0 || T < 0) return QZ_ERR_ARG;
+  if ((D & 1) != 0) return QZ_ERR_SHAPE;
+  if (B == 0 || S == 0 || D == 0) return 0;
+  if (!pos || !inv_freq || !cos || !sin || (T > 0 && (!cos_table || !sin_table))) return QZ_ERR_ARG;
+  RopeTableArgs a{};
+  a.pos = pos; a.pb = pos_b; a.ps = pos_s;
+  a.cos_t = cos_table; a.sin_t = sin_table; a.inv_freq = inv_freq;
+  a.cos = cos; a.sin = sin;
+  a.n = (long long)B * S * D; a.T = T; a.S = S; a.D = D; a.scale = scale;
+  const long long blocks = (a.n + 255) / 256;
+  if (blocks > 0x7FFFFFFFLL) return QZ_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case QZ_DT_F16: hipLaunchKernelGGL((k_rope_table<QZ_DT_F16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case QZ_DT_BF16: hipLaunchKernelGGL((k_rope_table<QZ_DT_BF16>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case QZ_DT_F32: hipLaunchKernelGGL((k_rope_table<QZ_DT_F32>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    default: return QZ_ERR_DTYPE;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_greedy_step(const void *logits, int dtype, int B, long long V, long long row, long long *hist,
+                              long long hist_row, long long hist_len, long long *pos, long long *tok, void *stream) {
+  if (B < 0 || V < 0 || row < 0 || hist_row < 0 || hist_len < 0) return QZ_ERR_ARG;
+  if (B == 0) return 0;
+  if (V == 0 || !logits || !hist || !pos || !tok || row < V || (B > 1 && hist_row < hist_len)) return QZ_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int esz = dtype == QZ_DT_F32 ? 4 : 2;
+  const bool vec = (V * esz) % 16 == 0 && (row * esz) % 16 == 0 && (uintptr_t)logits % 16 == 0;
+  switch (dtype) {
+    case QZ_DT_F16: hipLaunchKernelGGL((k_greedy_step<QZ_DT_F16>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
+    case QZ_DT_BF16: hipLaunchKernelGGL((k_greedy_step<QZ_DT_BF16>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
+    case QZ_DT_F32: hipLaunchKernelGGL((k_greedy_step<QZ_DT_F32>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
     default: return QZ_ERR_DTYPE;
   }
   return (int)hipGetLastError();

@@ -556,6 +556,112 @@ def unfuse_layer_ops(model: nn.Module) -> None:
 
 
 # ---------------------------------------------------------------------------
+# the host model's per-step glue around the decoder layers (not the Linear4bit path): the causal
+# mask and the rotary cos/sin, one launch each in place of the 7-9 small torch kernels each of them
+# costs a decode step (profiles/r5_decode_anatomy_8b.txt), with the same values
+# ---------------------------------------------------------------------------
+
+ROTARY_CLASSES = ("LlamaRotaryEmbedding", "MistralRotaryEmbedding", "Qwen2RotaryEmbedding")
+MODEL_CLASSES = ("LlamaModel", "MistralModel", "Qwen2Model")
+_MASK_PATCHED = {}  # modeling module name -> original create_causal_mask
+_ROPE_TABLE_MAX = 1 << 17
+
+
+def _table_rope_forward(mod: nn.Module, orig):
+    from .layer_ops import rope_table
+
+    def forward(x, position_ids, *args, **kw):
+        t = mod.__dict__.get("_qz_rope_tables", {}).get((x.dtype, x.device))
+        if t is None or args or kw or not (isinstance(position_ids, torch.Tensor) and position_ids.dim() == 2 and
+                                           position_ids.dtype == torch.int64 and position_ids.device == x.device):
+            return orig(x, position_ids, *args, **kw)
+        return rope_table(position_ids, t[0], t[1], mod.__dict__["_qz_inv_f32"], mod.attention_scaling)
+    return forward
+
+
+def _fast_causal_mask(orig):
+    from .layer_ops import decode_mask
+
+    def create_causal_mask(*args, **kw):
+        # one new token per sequence, keywords as LlamaModel.forward passes them, no padding mask,
+        # sdpa's bool mask, a static (compileable, non-sliding) cache: the mask is kv j <= q_offset
+        emb, pkv, cfg = kw.get("inputs_embeds"), kw.get("past_key_values"), kw.get("config")
+        if (not args and set(kw) <= {"config", "inputs_embeds", "attention_mask", "past_key_values", "position_ids"}
+                and kw.get("attention_mask") is None and cfg is not None and isinstance(emb, torch.Tensor)
+                and emb.is_cuda and emb.dim() == 3 and emb.shape[1] == 1 and pkv is not None
+                and getattr(cfg, "is_causal", True) and getattr(cfg, "_attn_implementation", None) == "sdpa"
+                and getattr(cfg, "sliding_window", None) is None and getattr(pkv, "is_compileable", False)
+                and not any(getattr(pkv, "is_sliding", ()))):
+            try:
+                q_off = pkv.get_query_offset(0)
+                kv_length, kv_offset = pkv.get_mask_sizes(1, 0)
+            except Exception:
+                q_off = kv_offset = None
+            if (isinstance(q_off, torch.Tensor) and q_off.dtype == torch.int64 and q_off.numel() == 1
+                    and q_off.device == emb.device and kv_offset == 0 and isinstance(kv_length, int)):
+                return decode_mask(q_off, emb.shape[0], kv_length)
+        return orig(*args, **kw)
+    create_causal_mask._qz_orig = orig
+    return create_causal_mask
+
+
+def fuse_decode_glue(model: nn.Module) -> int:
+    """Route a GPU model's rotary embedding through cos/sin tables its own forward computes once
+    here (positions 0..max_position_embeddings-1, the model's dtype; looked up by
+    layer_ops.rope_table) and its modeling module's create_causal_mask, for one new token against
+    a static cache, through layer_ops.decode_mask.  Everything else (CPU models, dynamic rope
+    types, padding masks, other caches) keeps transformers' own code.  Returns the number of
+    patches."""
+    import sys
+
+    n = 0
+    emb = model.get_input_embeddings() if hasattr(model, "get_input_embeddings") else None
+    dtype = emb.weight.dtype if emb is not None and hasattr(emb, "weight") else None
+    for m in model.modules():
+        if type(m).__name__ not in ROTARY_CLASSES or "_qz_rope_orig" in m.__dict__:
+            continue
+        inv = getattr(m, "inv_freq", None)
+        rt = str(getattr(m, "rope_type", "default"))
+        T = min(int(getattr(m, "max_seq_len_cached", 0) or 0), _ROPE_TABLE_MAX)
+        if (not isinstance(inv, torch.Tensor) or not inv.is_cuda or not inv.is_floating_point() or "dynamic" in rt
+                or rt == "longrope" or T <= 0 or dtype not in (torch.float16, torch.bfloat16, torch.float32)):
+            continue
+        orig = m.forward
+        with torch.no_grad():
+            cos, sin = orig(torch.empty(0, dtype=dtype, device=inv.device),
+                            torch.arange(T, device=inv.device).unsqueeze(0))
+        m.__dict__["_qz_rope_orig"] = orig
+        m.__dict__["_qz_inv_f32"] = inv.float().contiguous()   # what forward's .float() makes of it
+        m.__dict__["_qz_rope_tables"] = {(dtype, inv.device): (cos[0].contiguous(), sin[0].contiguous())}
+        m.__dict__["forward"] = _table_rope_forward(m, orig)
+        n += 1
+    for m in model.modules():
+        modname = type(m).__module__
+        if type(m).__name__ in MODEL_CLASSES and modname not in _MASK_PATCHED and n:
+            mod = sys.modules.get(modname)
+            fn = getattr(mod, "create_causal_mask", None) if mod is not None else None
+            if fn is not None:
+                _MASK_PATCHED[modname] = fn
+                setattr(mod, "create_causal_mask", _fast_causal_mask(fn))
+                n += 1
+    return n
+
+
+def unfuse_decode_glue(model: nn.Module) -> None:
+    """Undo fuse_decode_glue."""
+    import sys
+
+    for m in model.modules():
+        if m.__dict__.pop("_qz_rope_orig", None) is not None:
+            m.__dict__.pop("forward", None)
+            m.__dict__.pop("_qz_rope_tables", None)
+            m.__dict__.pop("_qz_inv_f32", None)
+    for modname, fn in list(_MASK_PATCHED.items()):
+        setattr(sys.modules[modname], "create_causal_mask", fn)
+        del _MASK_PATCHED[modname]
+
+
+# ---------------------------------------------------------------------------
 # pre-quantised checkpoints (SURVEY.md 8f row 1)
 # ---------------------------------------------------------------------------
 

@@ -189,3 +189,55 @@ def decode_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: tor
         out.data_ptr(), num_heads * D, work.data_ptr() if work is not None else None, float(scale),
         _lib.stream_of(q)), "qz_decode_attention")
     return out
+
+
+def decode_mask(q_offset: torch.Tensor, batch: int, kv_length: int) -> torch.Tensor:
+    """masking_utils.create_causal_mask's sdpa mask for one new token per sequence against a static
+    cache (no padding mask, kv_offset 0): bool [batch, 1, 1, kv_length], True where kv position
+    j <= q_offset (StaticLayer.cumulative_length, a device int64 read in-kernel)."""
+    if not (q_offset.is_cuda and q_offset.dtype == torch.int64 and q_offset.numel() == 1):
+        raise ValueError("decode_mask: q_offset must be one int64 on the GPU")
+    mask = torch.empty((batch, 1, 1, kv_length), dtype=torch.bool, device=q_offset.device)
+    _lib.check(_lib.lib.qz_decode_mask(q_offset.data_ptr(), batch, kv_length, mask.data_ptr(),
+                                       _lib.stream_of(q_offset)), "qz_decode_mask")
+    return mask
+
+
+def rope_table(position_ids: torch.Tensor, cos_t: torch.Tensor, sin_t: torch.Tensor, inv_freq: torch.Tensor,
+               scale: float):
+    """LlamaRotaryEmbedding.forward from tables: cos/sin [B, S, D] of position_ids [B, S] (int64)
+    copied from cos_t/sin_t [T, D] (what the module computed for positions 0..T-1); positions
+    outside the table computed in-kernel from inv_freq (fp32) and scale."""
+    if not (position_ids.is_cuda and position_ids.dtype == torch.int64 and position_ids.dim() == 2):
+        raise ValueError("rope_table: position_ids must be int64 [B, S] on the GPU")
+    T, D = cos_t.shape
+    if sin_t.shape != cos_t.shape or sin_t.dtype != cos_t.dtype or not (cos_t.is_contiguous() and sin_t.is_contiguous()):
+        raise ValueError("rope_table: cos/sin tables must be contiguous [T, D] of one dtype")
+    if inv_freq.dtype != torch.float32 or inv_freq.numel() * 2 != D or not inv_freq.is_contiguous():
+        raise ValueError("rope_table: inv_freq must be contiguous fp32 [D / 2]")
+    B, S = position_ids.shape
+    cos = torch.empty((B, S, D), dtype=cos_t.dtype, device=position_ids.device)
+    sin = torch.empty_like(cos)
+    _lib.check(_lib.lib.qz_rope_table(_lib.dtype_code(cos_t.dtype), B, S, D, position_ids.data_ptr(),
+                                      position_ids.stride(0), position_ids.stride(1), cos_t.data_ptr(),
+                                      sin_t.data_ptr(), T, inv_freq.data_ptr(), float(scale), cos.data_ptr(),
+                                      sin.data_ptr(), _lib.stream_of(position_ids)), "qz_rope_table")
+    return cos, sin
+
+
+def greedy_step(logits: torch.Tensor, hist: torch.Tensor, pos: torch.Tensor, tok: torch.Tensor) -> None:
+    """A decode loop's greedy pick and feedback in one launch: next = logits.argmax(-1) (torch's
+    order: NaN first, then the largest, the first index among equals) for logits [B, V] (rows of
+    any stride, unit element stride); hist[b, pos] = next[b]; tok[b] = next[b]; pos += 1.  hist
+    [B, H] contiguous int64, pos one int64, tok B contiguous int64, all on the logits' GPU."""
+    if logits.dim() != 2 or logits.stride(-1) != 1 or not logits.is_cuda:
+        raise ValueError("greedy_step: logits must be [B, V] on the GPU with unit element stride")
+    B, V = logits.shape
+    for t in (hist, pos, tok):
+        if t.dtype != torch.int64 or t.device != logits.device or not t.is_contiguous():
+            raise ValueError("greedy_step: hist/pos/tok must be contiguous int64 on the logits' device")
+    if hist.dim() != 2 or hist.shape[0] != B or pos.numel() != 1 or tok.numel() != B:
+        raise ValueError("greedy_step: hist [B, H], pos [1], tok [B]")
+    _lib.check(_lib.lib.qz_greedy_step(logits.data_ptr(), _lib.dtype_code(logits.dtype), B, V, logits.stride(0),
+                                       hist.data_ptr(), hist.shape[1], hist.shape[1], pos.data_ptr(), tok.data_ptr(),
+                                       _lib.stream_of(logits)), "qz_greedy_step")

@@ -203,7 +203,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
                          mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False,
-                         glue: bool = True):
+                         glue: bool = True, lm_head: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -244,6 +244,9 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
     if glue and layer_ops != "none":
         from quantizations_amd.integration import fuse_decode_glue
         n_layer_ops += fuse_decode_glue(model)   # the step's causal mask and rotary cos/sin: one launch each
+    if lm_head and layer_ops != "none":
+        from quantizations_amd.integration import fuse_lm_head
+        n_layer_ops += fuse_lm_head(model)   # the fp16 lm_head of a decode token: qz_gemv_dense
     return n_groups, n_layer_ops
 
 
@@ -1152,6 +1155,8 @@ def main():
                     help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
                          "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
                          "barriers cost more than launch boundaries, DESIGN.md section 12)")
+    ap.add_argument("--lm-head-library", action="store_true",
+                    help="keep the fp16 lm_head on F.linear (hipBLASLt) instead of layer_ops.gemv_dense")
     ap.add_argument("--no-glue", action="store_true",
                     help="keep transformers' own causal-mask and rotary code in the decode step (default: one "
                          "launch each, integration.fuse_decode_glue; same values)")
@@ -1267,7 +1272,8 @@ def main():
                                                      mlp_pair=not args.no_mlp_pair,
                                                      mlp_chain=args.mlp_chain,
                                                      qkv_attention=args.qkv_attention,
-                                                     glue=not args.no_glue)
+                                                     glue=not args.no_glue,
+                                                     lm_head=not args.lm_head_library)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1382,6 +1388,8 @@ def main():
         line["config"]["qkv_attention_launch"] = bool(args.qkv_attention and not args.no_attention
                                                       and not args.no_fuse and layer_ops in ("all", "all+decoder")
                                                       and not sharded)
+        line["config"]["lm_head"] = "F.linear (hipBLASLt)" if (args.lm_head_library or layer_ops == "none") \
+            else "layer_ops.gemv_dense"
         line["config"]["decode_glue_launches"] = bool(not args.no_glue and layer_ops != "none")
         line["config"]["greedy_argmax"] = {"kernel": "one launch with the feedback (layer_ops.greedy_step)",
                                            "two-stage": "two-stage (greedy_token)", "torch": "torch.argmax"}[GREEDY]

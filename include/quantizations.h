@@ -334,12 +334,18 @@ int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const v
  *   [B, S, D] contiguous copied from the [T, D] tables that module computed for positions 0..T-1;
  *   a position outside [0, T) is computed from inv_freq [D/2] (fp32 product, cosf/sinf, * scale,
  *   rounded to dtype).  D even; F16/BF16/F32. */
-/* qz_greedy_step: the greedy pick and its feedback, one workgroup: for b < B,
- *   next = argmax_v logits[b*row + v] (v < V; torch.argmax's order: NaN above every number,
- *   the first index among equals), hist[b*hist_row + *pos] = next, tok[b] = next; then *pos += 1.
- *   int64 hist/pos/tok on the device (graph-capturable); F16/BF16/F32 logits. */
+/* qz_greedy_step: the greedy pick and its feedback (two launches: 2048 logits per workgroup, then
+ *   one workgroup over the partials): for b < B, next = argmax_v logits[b*row + v] (v < V;
+ *   torch.argmax's order: NaN above every number, the first index among equals),
+ *   hist[b*hist_row + *pos] = next, tok[b] = next; then *pos += 1.  int64 hist/pos/tok on the
+ *   device (graph-capturable); F16/BF16/F32 logits; work: qz_greedy_step_work_bytes(B, V) bytes. */
+long long qz_greedy_step_work_bytes(int B, long long V);
 int qz_greedy_step(const void *logits, int dtype, int B, long long V, long long row, long long *hist,
-                   long long hist_row, long long hist_len, long long *pos, long long *tok, void *stream);
+                   long long hist_row, long long hist_len, long long *pos, long long *tok, void *work, void *stream);
+/* qz_gemv_dense: the model's fp16/bf16 lm_head for one decode token (transformers keeps it
+ *   unquantised): y[m] = sum_k W[m*K + k] x[k] for m < M, fp32 accumulation, rounded once to
+ *   dtype; K in {4096, 8192}, W and x 16-B aligned (else QZ_ERR_SHAPE, nothing launched). */
+int qz_gemv_dense(int M, int K, const void *x, int dtype, const void *W, void *y, void *stream);
 int qz_decode_mask(const long long *q_offset, int B, int L, void *mask, void *stream);
 int qz_rope_table(int dtype, int B, int S, int D, const long long *pos, long long pos_b, long long pos_s,
                   const void *cos_table, const void *sin_table, long long T, const float *inv_freq, float scale,

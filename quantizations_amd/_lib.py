@@ -80,7 +80,9 @@ SIGNATURES = {
     "qz_rope_qk": [_i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p],
     "qz_silu_mul": [_p, _p, _i, _ll, _p, _p],
     "qz_decode_mask": [_p, _i, _i, _p, _p],
-    "qz_greedy_step": [_p, _i, _i, _ll, _ll, _p, _ll, _ll, _p, _p, _p],
+    "qz_gemv_dense": [_i, _i, _p, _i, _p, _p, _p],
+    "qz_greedy_step": [_p, _i, _i, _ll, _ll, _p, _ll, _ll, _p, _p, _p, _p],
+    "qz_greedy_step_work_bytes": [_i, _ll],
     "qz_rope_table": [_i, _i, _i, _i, _p, _ll, _ll, _p, _p, _ll, _p, _f, _p, _p, _p],
     "qz_add_rmsnorm": [_p, _p, _i, _ll, _i, _ll, _p, _f, _p, _p, _ll, _p],
     "qz_bench_read_floor": [_p, _ll, _p, _p],
@@ -101,7 +103,8 @@ SIGNATURES = {
     "qz_mlp_chain_state_words": [],
     "qz_version": [],
 }
-RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll}
+RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll,
+            "qz_greedy_step_work_bytes": _ll}
 
 
 def _load():

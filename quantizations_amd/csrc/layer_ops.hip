@@ -353,77 +353,146 @@ template <int DT> __global__ __launch_bounds__(256) void k_rope_table(RopeTableA
 }
 
 // greedy pick + feedback of a decode step (bench.py's loop: next = argmax(logits[b]);
-// hist[b, *pos] = next; tok[b] = next; *pos += 1) in ONE workgroup: torch.argmax's order -- the
-// largest value, NaN above every number, the first index among equals
-constexpr int kGreedyThreads = 1024;
+// hist[b, *pos] = next; tok[b] = next; *pos += 1) in two launches: a partial pass in which each
+// workgroup reduces 2048 logits of a row (one 16-B vector per thread: one CU reads only ~25 GB/s, a
+// single workgroup over 128256 logits took 21 us), then one workgroup reduces the partials and
+// writes the feedback.  torch.argmax's order: the largest value, NaN above every number, the first
+// index among equals (a total order on (value, index), so any reduction tree gives the same pick)
+constexpr int kGreedyChunk = 2048;
 __device__ __forceinline__ bool greedy_better(float v, long long i, float w, long long j) {
   const bool vn = v != v, wn = w != w;
   if (vn || wn) return vn && (!wn || i < j);
   return v > w || (v == w && i < j);
 }
-template <int DT>
-__global__ __launch_bounds__(kGreedyThreads) void k_greedy_step(const void *logits, long long row, int B, long long V,
-                                                                long long *hist, long long hist_row, long long *pos,
-                                                                long long *tok, bool vec) {
-  __shared__ float s_v[kGreedyThreads / 64];
-  __shared__ long long s_i[kGreedyThreads / 64];
+// (best, bi) over the workgroup (256 threads) -> thread 0; bi == none marks "no element"
+__device__ __forceinline__ void greedy_reduce_wg(float &best, long long &bi, long long none, float *s_v,
+                                                 long long *s_i) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    const float w = __shfl_xor(best, o);
+    const long long j = __shfl_xor(bi, o);
+    if (j != none && (bi == none || greedy_better(w, j, best, bi))) { best = w; bi = j; }
+  }
+  if (lane == 0) { s_v[wave] = best; s_i[wave] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (s_i[w] != none && (bi == none || greedy_better(s_v[w], s_i[w], best, bi))) { best = s_v[w]; bi = s_i[w]; }
+  }
+  __syncthreads();
+}
+template <int DT>
+__global__ __launch_bounds__(256) void k_greedy_partial(const void *logits, long long row, long long V, int nb,
+                                                        float *pv, long long *pi, bool vec) {
+  __shared__ float s_v[4];
+  __shared__ long long s_i[4];
+  const int tid = threadIdx.x, b = blockIdx.y;
+  const long long base = (long long)blockIdx.x * kGreedyChunk;
+  const long long end = base + kGreedyChunk < V ? base + kGreedyChunk : V;
+  const void *lr = reinterpret_cast<const unsigned char *>(logits) + (size_t)b * row * (DT == QZ_DT_F32 ? 4 : 2);
+  float best = -__builtin_inff();
+  long long bi = V;   // no element yet
+  constexpr int E = DT == QZ_DT_F32 ? 4 : 8;   // elements per 16-B vector
+  if (vec) {
+    // 2048 / E vectors per workgroup: at most 256 / (8 / E) per thread, in increasing index order
+    typedef uint32_t w4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int u = 0; u < kGreedyChunk / E / 256; ++u) {
+      const long long i0 = base + (long long)(tid + 256 * u) * E;
+      if (i0 < end) {
+        const w4_t r = *reinterpret_cast<const w4_t *>(reinterpret_cast<const unsigned char *>(lr) +
+                                                        i0 * (DT == QZ_DT_F32 ? 4 : 2));
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t w = r[DT == QZ_DT_F32 ? e : e >> 1];
+          float v;
+          if constexpr (DT == QZ_DT_F32) v = __uint_as_float(w);
+          else if constexpr (DT == QZ_DT_F16) v = __half2float(__ushort_as_half((unsigned short)((e & 1) ? w >> 16 : w & 0xFFFFu)));
+          else v = __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
+          if (v > best || (v != v && best == best) || bi == V) { best = v; bi = i0 + e; }
+        }
+      }
+    }
+  } else {
+    for (long long i = base + tid; i < end; i += 256) {
+      const float v = load_f32<DT>(lr, i);
+      if (v > best || (v != v && best == best) || bi == V) { best = v; bi = i; }
+    }
+  }
+  greedy_reduce_wg(best, bi, V, s_v, s_i);
+  if (tid == 0) {
+    pv[(size_t)b * nb + blockIdx.x] = best;
+    pi[(size_t)b * nb + blockIdx.x] = bi;
+  }
+}
+__global__ __launch_bounds__(256) void k_greedy_final(int B, long long V, int nb, const float *pv,
+                                                      const long long *pi, long long *hist, long long hist_row,
+                                                      long long *pos, long long *tok) {
+  __shared__ float s_v[4];
+  __shared__ long long s_i[4];
+  const int tid = threadIdx.x;
   const long long p = *pos;
   for (int b = 0; b < B; ++b) {
-    const void *lr = reinterpret_cast<const unsigned char *>(logits) + (size_t)b * row * (DT == QZ_DT_F32 ? 4 : 2);
     float best = -__builtin_inff();
-    long long bi = V;   // no element yet
-    constexpr int E = DT == QZ_DT_F32 ? 4 : 8;   // elements per 16-B vector
-    if (vec) {
-      // 16-B loads, all of a thread's (up to 16: 128256 fp16 logits) in flight at once; a thread
-      // visits its elements in increasing index order, so a later equal value never replaces
-      typedef uint32_t w4_t __attribute__((ext_vector_type(4)));
-      const w4_t *vr = reinterpret_cast<const w4_t *>(lr);
-      const long long nv = V / E;
-      constexpr int U = 16;
-      for (long long q0 = tid; q0 < nv; q0 += (long long)U * kGreedyThreads) {
-        w4_t r[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long q = q0 + (long long)u * kGreedyThreads;
-          r[u] = q < nv ? vr[q] : w4_t{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const long long q = q0 + (long long)u * kGreedyThreads;
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const uint32_t w = r[u][DT == QZ_DT_F32 ? e : e >> 1];
-            float v;
-            if constexpr (DT == QZ_DT_F32) v = __uint_as_float(w);
-            else if constexpr (DT == QZ_DT_F16) v = __half2float(__ushort_as_half((unsigned short)((e & 1) ? w >> 16 : w & 0xFFFFu)));
-            else v = __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
-            if (q < nv && (v > best || (v != v && best == best) || bi == V)) { best = v; bi = q * E + e; }
-          }
-        }
-      }
-    } else {
-      for (long long i = tid; i < V; i += kGreedyThreads) {
-        const float v = load_f32<DT>(lr, i);
-        if (bi == V || greedy_better(v, i, best, bi)) { best = v; bi = i; }
-      }
+    long long bi = V;
+    for (int c = tid; c < nb; c += 256) {
+      const float v = pv[(size_t)b * nb + c];
+      const long long i = pi[(size_t)b * nb + c];
+      if (i != V && (bi == V || greedy_better(v, i, best, bi))) { best = v; bi = i; }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      const float w = __shfl_xor(best, o);
-      const long long j = __shfl_xor(bi, o);
-      if (j != V && (bi == V || greedy_better(w, j, best, bi))) { best = w; bi = j; }
-    }
-    if (lane == 0) { s_v[wave] = best; s_i[wave] = bi; }
-    __syncthreads();
+    greedy_reduce_wg(best, bi, V, s_v, s_i);
     if (tid == 0) {
-      for (int w = 1; w < kGreedyThreads / 64; ++w)
-        if (s_i[w] != V && (bi == V || greedy_better(s_v[w], s_i[w], best, bi))) { best = s_v[w]; bi = s_i[w]; }
       hist[(size_t)b * hist_row + p] = bi;
       tok[b] = bi;
     }
-    __syncthreads();
   }
   if (tid == 0) *pos = p + 1;
+}
+
+// ---- the host model's fp16 / bf16 lm_head for one decode token (not 4-bit: transformers keeps it
+// in the model dtype): y[m] = sum_k W[m, k] x[k], fp32 accumulation, rounded once.  Each wave owns
+// R rows; lane l reads the 16-B chunks l, l + 64, ... of a row (KCH = K / 512 of them) with
+// non-temporal loads, all R * KCH in flight before the first dot product; x's chunks stay in
+// registers; a butterfly over the 64 lanes ends each row ----
+template <int DT, int KCH, int R>
+__global__ __launch_bounds__(256) void k_gemv_dense(const void *__restrict__ W, const void *__restrict__ x, int M,
+                                                    int K, void *__restrict__ y) {
+  typedef uint32_t w4_t __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long row0 = ((long long)blockIdx.x * 4 + wave) * R;
+  if (row0 >= M) return;
+  w4_t xv[KCH];
+#pragma unroll
+  for (int j = 0; j < KCH; ++j) xv[j] = reinterpret_cast<const w4_t *>(x)[lane + 64 * j];
+  w4_t wv[R][KCH];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const long long row = row0 + r < M ? row0 + r : M - 1;
+    const w4_t *wr = reinterpret_cast<const w4_t *>(reinterpret_cast<const uint16_t *>(W) + row * K);
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) wv[r][j] = __builtin_nontemporal_load(wr + lane + 64 * j);
+  }
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float a = 0.0f;
+#pragma unroll
+    for (int j = 0; j < KCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a = dot2_dt<DT>(wv[r][j][e], xv[j][e], a);
+    acc[r] = a;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[r] += __shfl_xor(acc[r], o);
+  }
+  if (lane < R && row0 + lane < M) {
+    float v = acc[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) v = lane == r ? acc[r] : v;
+    store_f32<DT>(y, row0 + lane, v);
+  }
 }
 
 }  // namespace
@@ -571,19 +640,52 @@ extern "C" int qz_rope_table(int dtype, int B, int S, int D, const long long *po
   return (int)hipGetLastError();
 }
 
+extern "C" long long qz_greedy_step_work_bytes(int B, long long V) {
+  if (B <= 0 || V <= 0) return 0;
+  return (long long)B * ((V + kGreedyChunk - 1) / kGreedyChunk) * 16;
+}
+
 extern "C" int qz_greedy_step(const void *logits, int dtype, int B, long long V, long long row, long long *hist,
-                              long long hist_row, long long hist_len, long long *pos, long long *tok, void *stream) {
+                              long long hist_row, long long hist_len, long long *pos, long long *tok, void *work,
+                              void *stream) {
   if (B < 0 || V < 0 || row < 0 || hist_row < 0 || hist_len < 0) return QZ_ERR_ARG;
   if (B == 0) return 0;
-  if (V == 0 || !logits || !hist || !pos || !tok || row < V || (B > 1 && hist_row < hist_len)) return QZ_ERR_ARG;
+  if (V == 0 || !logits || !hist || !pos || !tok || !work || row < V || (B > 1 && hist_row < hist_len))
+    return QZ_ERR_ARG;
+  const long long nbl = (V + kGreedyChunk - 1) / kGreedyChunk;
+  if (nbl > 0x7FFFFFFFLL || B > 65535) return QZ_ERR_SHAPE;
+  const int nb = (int)nbl;
+  float *pv = reinterpret_cast<float *>(work);
+  long long *pi = reinterpret_cast<long long *>(reinterpret_cast<unsigned char *>(work) + (size_t)B * nb * 8);
   hipStream_t s = (hipStream_t)stream;
   const int esz = dtype == QZ_DT_F32 ? 4 : 2;
   const bool vec = (V * esz) % 16 == 0 && (row * esz) % 16 == 0 && (uintptr_t)logits % 16 == 0;
+  const dim3 g((unsigned)nb, (unsigned)B);
   switch (dtype) {
-    case QZ_DT_F16: hipLaunchKernelGGL((k_greedy_step<QZ_DT_F16>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
-    case QZ_DT_BF16: hipLaunchKernelGGL((k_greedy_step<QZ_DT_BF16>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
-    case QZ_DT_F32: hipLaunchKernelGGL((k_greedy_step<QZ_DT_F32>), dim3(1), dim3(kGreedyThreads), 0, s, logits, row, B, V, hist, hist_row, pos, tok, vec); break;
+    case QZ_DT_F16: hipLaunchKernelGGL((k_greedy_partial<QZ_DT_F16>), g, dim3(256), 0, s, logits, row, V, nb, pv, pi, vec); break;
+    case QZ_DT_BF16: hipLaunchKernelGGL((k_greedy_partial<QZ_DT_BF16>), g, dim3(256), 0, s, logits, row, V, nb, pv, pi, vec); break;
+    case QZ_DT_F32: hipLaunchKernelGGL((k_greedy_partial<QZ_DT_F32>), g, dim3(256), 0, s, logits, row, V, nb, pv, pi, vec); break;
     default: return QZ_ERR_DTYPE;
+  }
+  hipLaunchKernelGGL(k_greedy_final, dim3(1), dim3(256), 0, s, B, V, nb, pv, pi, hist, hist_row, pos, tok);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qz_gemv_dense(int M, int K, const void *x, int dtype, const void *W, void *y, void *stream) {
+  if (M < 0 || K < 0) return QZ_ERR_ARG;
+  if (M == 0) return 0;
+  if (!x || !W || !y) return QZ_ERR_ARG;
+  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_DTYPE;
+  if ((K != 4096 && K != 8192) || ((uintptr_t)x | (uintptr_t)W) % 16 != 0) return QZ_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 4096) {
+    const dim3 g((unsigned)((M + 15) / 16));
+    if (dtype == QZ_DT_F16) hipLaunchKernelGGL((k_gemv_dense<QZ_DT_F16, 8, 4>), g, dim3(256), 0, s, W, x, M, K, y);
+    else hipLaunchKernelGGL((k_gemv_dense<QZ_DT_BF16, 8, 4>), g, dim3(256), 0, s, W, x, M, K, y);
+  } else {
+    const dim3 g((unsigned)((M + 7) / 8));
+    if (dtype == QZ_DT_F16) hipLaunchKernelGGL((k_gemv_dense<QZ_DT_F16, 16, 2>), g, dim3(256), 0, s, W, x, M, K, y);
+    else hipLaunchKernelGGL((k_gemv_dense<QZ_DT_BF16, 16, 2>), g, dim3(256), 0, s, W, x, M, K, y);
   }
   return (int)hipGetLastError();
 }

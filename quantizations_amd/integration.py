@@ -647,6 +647,33 @@ def fuse_decode_glue(model: nn.Module) -> int:
     return n
 
 
+def fuse_lm_head(model: nn.Module) -> int:
+    """Route the model's unquantised fp16/bf16 output projection (get_output_embeddings(), no bias)
+    through layer_ops.gemv_dense for a single decode token (6.8 vs 5.7 TB/s for hipBLASLt at
+    128256 x 4096, profiles/r5_lm_head_times.txt); every other input keeps F.linear.  Returns 1 if
+    patched."""
+    head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+    if not isinstance(head, nn.Linear) or head.bias is not None or "_qz_dense_head" in head.__dict__:
+        return 0
+    from .layer_ops import gemv_dense, gemv_dense_supported
+
+    orig = head.forward
+
+    def forward(x):
+        if gemv_dense_supported(x, head.weight):
+            return gemv_dense(x, head.weight)
+        return orig(x)
+    head.__dict__["forward"] = forward
+    head.__dict__["_qz_dense_head"] = True
+    return 1
+
+
+def unfuse_lm_head(model: nn.Module) -> None:
+    head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+    if head is not None and head.__dict__.pop("_qz_dense_head", None):
+        head.__dict__.pop("forward", None)
+
+
 def unfuse_decode_glue(model: nn.Module) -> None:
     """Undo fuse_decode_glue."""
     import sys

@@ -226,7 +226,7 @@ def rope_table(position_ids: torch.Tensor, cos_t: torch.Tensor, sin_t: torch.Ten
 
 
 def greedy_step(logits: torch.Tensor, hist: torch.Tensor, pos: torch.Tensor, tok: torch.Tensor) -> None:
-    """A decode loop's greedy pick and feedback in one launch: next = logits.argmax(-1) (torch's
+    """A decode loop's greedy pick and feedback in two launches (qz_greedy_step): next = logits.argmax(-1) (torch's
     order: NaN first, then the largest, the first index among equals) for logits [B, V] (rows of
     any stride, unit element stride); hist[b, pos] = next[b]; tok[b] = next[b]; pos += 1.  hist
     [B, H] contiguous int64, pos one int64, tok B contiguous int64, all on the logits' GPU."""
@@ -238,6 +238,32 @@ def greedy_step(logits: torch.Tensor, hist: torch.Tensor, pos: torch.Tensor, tok
             raise ValueError("greedy_step: hist/pos/tok must be contiguous int64 on the logits' device")
     if hist.dim() != 2 or hist.shape[0] != B or pos.numel() != 1 or tok.numel() != B:
         raise ValueError("greedy_step: hist [B, H], pos [1], tok [B]")
+    work = torch.empty(_lib.lib.qz_greedy_step_work_bytes(B, V), dtype=torch.uint8, device=logits.device)
     _lib.check(_lib.lib.qz_greedy_step(logits.data_ptr(), _lib.dtype_code(logits.dtype), B, V, logits.stride(0),
                                        hist.data_ptr(), hist.shape[1], hist.shape[1], pos.data_ptr(), tok.data_ptr(),
-                                       _lib.stream_of(logits)), "qz_greedy_step")
+                                       work.data_ptr(), _lib.stream_of(logits)), "qz_greedy_step")
+
+
+DENSE_K = (4096, 8192)   # the widths qz_gemv_dense takes (Llama-3 8B / 70B)
+
+
+def gemv_dense_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """One token through an unquantised fp16/bf16 [M, K] weight (the lm_head) with qz_gemv_dense."""
+    if not (x.is_cuda and weight.is_cuda and x.device == weight.device and x.dtype == weight.dtype
+            and x.dtype in (torch.float16, torch.bfloat16) and weight.dim() == 2 and weight.is_contiguous()):
+        return False
+    K = weight.shape[1]
+    return (K in DENSE_K and x.shape[-1] == K and x.numel() == K and x.is_contiguous()
+            and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0 and weight.shape[0] < 2 ** 31)
+
+
+def gemv_dense(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """F.linear(x, weight) for one token ([..., K] with one row) -- fp32 accumulation, rounded once
+    (the library's numerics class; the summation order differs)."""
+    if not gemv_dense_supported(x, weight):
+        raise ValueError("gemv_dense: unsupported shapes/dtypes/layout")
+    M, K = weight.shape
+    y = torch.empty((*x.shape[:-1], M), dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib.qz_gemv_dense(M, K, x.data_ptr(), _lib.dtype_code(x.dtype), weight.data_ptr(), y.data_ptr(),
+                                      _lib.stream_of(x)), "qz_gemv_dense")
+    return y

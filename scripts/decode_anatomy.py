@@ -3,8 +3,9 @@
   rocprofv3 --kernel-trace -d DIR -- python3 bench.py --steps 8 --warmup 4 --no-prefill --no-cpu --no-roofline
   python scripts/decode_anatomy.py DIR [--steps 4]
 
-A decode step ends with the argmax reduction of the logits; the last `--steps` complete
-steps (argmax to argmax) are averaged.  Under the tracer every dispatch carries its own
+A decode step ends with the greedy pick of the logits (k_greedy_final, or torch's ArgMax reduction
+for bench.py --greedy two-stage/torch); the last `--steps` complete steps (pick to pick) are
+averaged.  Under the tracer every dispatch carries its own
 extra cost, so the absolute times are inflated; the launch COUNT per step is exact.
 """
 import argparse
@@ -25,9 +26,10 @@ def main():
             for r in csv.DictReader(fh):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if "ArgMax" in r[2]]
+    ends = [i for i, r in enumerate(rows) if "k_greedy_final" in r[2]] or \
+        [i for i, r in enumerate(rows) if "ArgMax" in r[2]]
     if len(ends) < a.steps + 1:
-        raise SystemExit(f"only {len(ends)} argmax dispatches found")
+        raise SystemExit(f"only {len(ends)} greedy-pick dispatches found")
     sel = ends[-(a.steps + 1):]
     per = defaultdict(lambda: [0, 0.0])
     walls, counts = [], []

@@ -171,3 +171,66 @@ def test_greedy_step_is_torch_argmax_and_feedback(dtype, B, V):
         torch.cuda.synchronize()
         assert torch.equal(tok, tok_r), (i, tok, tok_r)
         assert torch.equal(hist, hist_r) and torch.equal(pos, pos_r)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,K", [(5000, 4096), (4099, 8192), (17, 4096), (1, 8192)])
+def test_gemv_dense_against_fp64_and_library(dtype, M, K):
+    """qz_gemv_dense (the lm_head of a decode token): fp32 accumulation rounded once -- the library's
+    numerics class.  Its error against an fp64 product is the output rounding (within 5 % of
+    F.linear's), and it differs from F.linear by at most one rounding step where it differs."""
+    import torch.nn.functional as F
+
+    from quantizations_amd.layer_ops import gemv_dense, gemv_dense_supported
+
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    W = (torch.randn(M, K, device=DEV, generator=g) * 0.02).to(dtype)
+    x = torch.randn(1, 1, K, device=DEV, generator=g).to(dtype)
+    assert gemv_dense_supported(x, W)
+    y = gemv_dense(x, W)
+    yl = F.linear(x, W)
+    ref = W.double() @ x.view(-1).double()
+    assert y.shape == yl.shape == (1, 1, M) and y.dtype == dtype
+    e_o = ((y.view(-1).double() - ref).norm() / ref.norm()).item()
+    e_l = ((yl.view(-1).double() - ref).norm() / ref.norm()).item()
+    assert e_o <= 1.05 * e_l + 1e-6, (e_o, e_l)
+    ulp = torch.finfo(dtype).eps
+    assert torch.all((y.float() - yl.float()).abs() <= 2 * ulp * yl.float().abs().clamp_min(1e-3))
+    # two rows, a misaligned x or another width: the caller keeps F.linear
+    assert not gemv_dense_supported(torch.randn(2, 1, K, device=DEV).to(dtype), W)
+    assert not gemv_dense_supported(torch.randn(1, 1, K + 1, device=DEV).to(dtype)[..., 1:], W)
+
+
+def test_llama_decode_dense_lm_head_tokens():
+    """bench.py's graph decode of a 4096-wide model with the lm_head on qz_gemv_dense (its default)
+    against F.linear: identical greedy tokens; the dense launch ran."""
+    from transformers import LlamaForCausalLM
+
+    import bench
+    from quantizations_amd import _lib
+    from quantizations_amd.integration import replace_with_bnb_linear, unfuse_layer_ops, unfuse_lm_head
+
+    cfg = _cfg("llama3", max_pos=256, hidden=4096, heads=32, kv=8, layers=1)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    replace_with_bnb_linear(model, modules_to_not_convert=["lm_head"], quant_type="nf4",
+                            compute_dtype=torch.float32)
+    bench.prepare_decode_model(model, 0, 1, False)
+    calls = {"n": 0}
+    fn = _lib.lib.qz_gemv_dense
+
+    def spy(*a):
+        calls["n"] += 1
+        return fn(*a)
+    _lib.lib.qz_gemv_dense = spy
+    try:
+        _, hist = bench.decode_bench_graph(model, cfg, steps=6, warmup=2, prompt_len=8, world=1, batch=1)
+    finally:
+        _lib.lib.qz_gemv_dense = fn
+    assert calls["n"] >= 1
+    unfuse_lm_head(model)
+    try:
+        _, ref_hist = bench.decode_bench_graph(model, cfg, steps=6, warmup=2, prompt_len=8, world=1, batch=1)
+    finally:
+        unfuse_layer_ops(model)
+    assert torch.equal(hist, ref_hist)

@@ -38,3 +38,8 @@ t_plain = graph_time(lambda i: gemv_4bit_grouped(x, it(i % NC), exact_codes=True
 t_o = graph_time(lambda i: gemv_4bit(x, o[i % NC][0], state=o[i % NC][1], exact_codes=True, residual=res))
 print(f"70B q/k/v: fused norm {t_fused:.2f} us, norm launch + grouped {t_two:.2f} us, grouped alone {t_plain:.2f} us;"
       f" o_proj + residual {t_o:.2f} us (b2b in one graph)", flush=True)
+
+
+# (measured once with a QZ_GROUPED_NORM_WK1 knob, since removed: whole rows per wave with the fused
+#  prologue at R = 4 / 2 / 1 took 16.37 / 16.96 / 23.40 us against 16.61 for the norm launch + the
+#  K-split grouped launch -- profiles/r5_qkv70_forms.txt)

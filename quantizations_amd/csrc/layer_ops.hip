@@ -82,6 +82,10 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const void *__restrict__ x, con
 // so a row costs one memory round trip before the reduction instead of one per loop iteration and
 // pass (the Llama-3-70B norm, K = 8192: 8.3 us as the loop, profiles/r5_pair_k8192_ab.txt).  Same
 // per-thread element order, same reduction, same roundings: bit-identical to k_rmsnorm.
+// gridDim.y > 1 (a few rows, e.g. one decode token): workgroup (row, sl) of the gridDim.y slices
+// computes the row's whole sum of squares (the same bits in every slice) but loads the weight for,
+// and writes, only the chunks c with c % gridDim.y == sl -- one CU streams only ~25 GB/s, so the
+// row's output is spread over several CUs
 template <int DT, bool ADD>
 __global__ __launch_bounds__(256) void k_rmsnorm_held(const void *__restrict__ x, const void *__restrict__ r, int K,
                                                       long long ldx, const void *__restrict__ w, float eps,
@@ -106,10 +110,11 @@ __global__ __launch_bounds__(256) void k_rmsnorm_held(const void *__restrict__ x
       if constexpr (ADD) ra[c] = rr[i];
     }
   }
+  const int nsl = (int)gridDim.y, sl = (int)blockIdx.y;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int i = (int)threadIdx.x + 256 * c;
-    if (i < nv) wa[c] = wr[i];
+    if (i < nv && c % nsl == sl) wa[c] = wr[i];
   }
   float h[NC][V];
   float ss = 0.0f;
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm_held(const void *__restrict__ x
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int i = (int)threadIdx.x + 256 * c;
-    if (i < nv) {
+    if (i < nv && c % nsl == sl) {
       uint4 ov, sv;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
@@ -273,8 +278,13 @@ void launch_rmsnorm(bool vec, long long rows, const void *x, const void *r, int 
                     float eps, void *y, void *sum, long long ldy, hipStream_t s) {
   const dim3 g((unsigned)rows), b(256);
   constexpr int V = DT == QZ_DT_F32 ? 4 : 8;
-  if (vec && K / V <= 256 * 8)
-    hipLaunchKernelGGL((k_rmsnorm_held<DT, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
+  if (vec && K / V <= 256 * 8) {
+    // a few rows: each row's chunks over up to 8 workgroups (one per 256-vector chunk)
+    const int nc = (K / V + 255) / 256;
+    const int nsl = rows * nc <= 64 ? nc : 1;
+    hipLaunchKernelGGL((k_rmsnorm_held<DT, ADD>), dim3((unsigned)rows, (unsigned)nsl), b, 0, s, x, r, K, ldx, w, eps,
+                       y, sum, ldy);
+  }
   else if (vec) hipLaunchKernelGGL((k_rmsnorm<DT, true, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
   else hipLaunchKernelGGL((k_rmsnorm<DT, false, ADD>), g, b, 0, s, x, r, K, ldx, w, eps, y, sum, ldy);
 }

@@ -196,9 +196,6 @@ int qz_gemm_4bit_grouped(int nseg, const qz_gemv_segment *segs, int T, int K, co
  * 16-B aligned X/W/Y, row strides % 8 == 0, 32-bit byte offsets), else QZ_ERR_SHAPE. */
 int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dtype, const void *W, const void *bias, void *Y,
                   int ldy, void *stream);
-/* qz_gemm_16bit on the persistent epilogue-overlap kernel (measurement twin; same outputs). */
-int qz_gemm_16bit_persistent(int T, int M, int K, const void *X, int ldx, int dtype, const void *W, const void *bias,
-                             void *Y, int ldy, void *stream);
 int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy);
 
 /* Workspace bytes qz_gemm_4bit uses for (T, M, K) at its preferred K split

@@ -68,7 +68,6 @@ SIGNATURES = {
     "qz_gemm_4bit": [_i, _i, _i, _p, _i, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p, _ll, _p],
     "qz_gemm_4bit_workspace_size": [_i, _i, _i],
     "qz_gemm_16bit": [_i, _i, _i, _p, _i, _i, _p, _p, _p, _i, _p],
-    "qz_gemm_16bit_persistent": [_i, _i, _i, _p, _i, _i, _p, _p, _p, _i, _p],
     "qz_gemm_16bit_ok": [_i, _i, _i, _p, _i, _p, _p, _i],
     "qz_gemm_4bit_grouped": [_i, _p, _i, _i, _p, _i, _i, _i, _i, _i, _p],
     "qz_quantize_4bit": [_p, _i, _ll, _i, _i, _p, _p, _p],

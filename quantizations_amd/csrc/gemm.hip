@@ -1478,195 +1478,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_gemm16_4e: k_gemm16_4d's schedule (16x16x32, P1 = 16, P2 = 112, grouped XCD-aware order) in a
-// persistent workgroup, so one tile's epilogue overlaps the next tile's first loads: the quadrant
-// goes through the LDS image as in 4d, every lane reads its 32 output vectors into registers, one
-// barrier frees the LDS, then the 32 global stores go out FIRST and the next tile's steps 0 and 1
-// are staged behind them -- the stores drain while the DMAs are in flight (one vmcnt wait covers
-// both), instead of ending the workgroup.  XCD x's workgroups walk the x-th eighth of the grouped
-// tile order with stride (workgroups per XCD), so the 32 tiles an XCD holds at once are the same
-// neighbourhood 4d's dispatch order gives it.  Grid: a multiple of 8, at most the tile count.
-template <int DT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4e(GemmParams p) {
-  constexpr int P1 = 16, P2 = 112, kNM = 128;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[k4dLds];
-  typedef __attribute__((address_space(3))) void *lds_ptr_t;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wt = wave >> 1, wm = wave & 1;
-
-  const int tiles_m = (p.M + k4wM - 1) / k4wM, tiles_t = (p.T + k4wT - 1) / k4wT;
-  const int ntiles = tiles_m * tiles_t;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, per_xcd = nwg >> 3, jx = bid >> 3;
-  const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int xb = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int xe = xb + q8 + (xcd < r8 ? 1 : 0);
-  const bool grouped = tiles_m % 8 == 0 && tiles_t % 4 == 0;
-  auto tile_of = [&](int wg, int &m0, int &t0) {
-    int tm = wg % tiles_m, tt = wg / tiles_m;
-    if (grouped) {
-      const int grp = wg / (4 * tiles_m), r = wg % (4 * tiles_m);
-      tt = 4 * grp + (r % 32) / 8;
-      tm = 8 * (r / 32) + r % 8;
-    }
-    m0 = tm * k4wM;
-    t0 = tt * k4wT;
-  };
-  const int nsteps = p.K / kBK;
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void *>(p.X), (short)0, (int)((uint32_t)p.T * (uint32_t)p.ldx * 2u), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned char *>(p.B), (short)0, (int)((uint32_t)p.M * (uint32_t)p.K * 2u), 0x00020000);
-  const uint32_t sw = (uint32_t)((tid & 7) ^ ((tid >> 4) & 7));
-  uint32_t xo[8], wo[8];
-  auto set_offsets = [&](int m0, int t0) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int row = 32 * c + (tid >> 3);
-      xo[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * sw) * 2u;
-      wo[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sw) * 2u;
-    }
-  };
-  auto dma_half = [&](int step, int buf, int c, int h) {
-    const int kb = step * (kBK * 2);
-    unsigned char *d = smem + buf * k4dBuf + 4096 * c + 1024 * wave;
-    if (h == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)d, 16, xo[c], kb, 0, 0);
-    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(d + k4wStage), 16, wo[c], kb, 0, 0);
-  };
-  const int fr = lane & 15, fk = lane >> 4;
-  const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
-                          (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
-  v4u xf[2][8], wf[2][8];
-  auto frag_read = [&](int buf, int kk, int g) {
-    const unsigned char *bx = smem + buf * k4dBuf + fl[kk];
-    const int wj = g == 0 ? 0 : g - 8;
-    if (g >= 1 && g <= 8) xf[kk][g - 1] = *reinterpret_cast<const v4u *>(bx + (128 * wt + 16 * (g - 1)) * 128);
-    else wf[kk][wj] = *reinterpret_cast<const v4u *>(bx + k4wStage + (128 * wm + 16 * wj) * 128);
-  };
-  f4_t acc[8][8];
-  auto mfma = [&](int kk, int n) {
-    const int j = n >> 3, i = n & 7;
-    if constexpr (DT == QZ_DT_F16)
-      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, wf[kk][j]),
-                                                         __builtin_bit_cast(h8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
-    else
-      acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8_t, wf[kk][j]),
-                                                          __builtin_bit_cast(b8_t, xf[kk][i]), acc[j][i], 0, 0, 0);
-  };
-  constexpr int kR1 = P1 / 16, kD = (P2 - P1) / 16, kR0 = (kNM - P2) / 16;
-
-  int wg = xb + jx;
-  if (wg >= xe) return;
-  int m0, t0;
-  tile_of(wg, m0, t0);
-  set_offsets(m0, t0);
-  // first tile's prologue: steps 0 and 1 in flight, step 0's k-half 0 in registers
-#pragma unroll
-  for (int c = 0; c < 8; ++c) { dma_half(0, 0, c, 0); dma_half(0, 0, c, 1); }
-#pragma unroll
-  for (int c = 0; c < 8; ++c) { dma_half(min(1, nsteps - 1), 1, c, 0); dma_half(min(1, nsteps - 1), 1, c, 1); }
-  __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int g = 0; g < 16; ++g) frag_read(0, 0, g);
-
-  for (;;) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] = f4_t{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < nsteps; ++s) {
-      const int b = s & 1;
-      const int s2 = min(s + 2, nsteps - 1);
-      static_for<kNM>([&](auto nc) {
-        constexpr int n = decltype(nc)::value;
-        mfma(n / (kNM / 2), n % (kNM / 2));
-        if constexpr (n < P1) {
-          if constexpr ((n + 1) % kR1 == 0) {
-            frag_read(b, 1, (n + 1) / kR1 - 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          if constexpr (n == P1 - 1) {
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        } else if constexpr (n < P2) {
-          if constexpr ((n + 1 - P1) % kD == 0) {
-            constexpr int d = (n + 1 - P1) / kD - 1;
-            dma_half(s2, b, d >> 1, d & 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          if constexpr (n == P2 - 1) {
-            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        } else if constexpr ((n + 1 - P2) % kR0 == 0) {
-          frag_read(b ^ 1, 0, (n + 1 - P2) / kR0 - 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      });
-    }
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-
-    // epilogue: quadrant -> LDS image (+ bias) -> 32 row vectors per lane in registers
-    __syncthreads();
-    unsigned char *ew = smem + wave * (128 * k4wERow);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float bv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        bv[r] = p.bias ? load_f32<DT>(p.bias, min(m0 + 128 * wm + 16 * j + 4 * fk + r, p.M - 1)) : 0.0f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const f4_t v = acc[j][i];
-        const uint32_t l2 = cvt_pk16<DT>(v[0] + bv[0], v[1] + bv[1]);
-        const uint32_t h2 = cvt_pk16<DT>(v[2] + bv[2], v[3] + bv[3]);
-        *reinterpret_cast<uint2 *>(ew + (16 * i + fr) * k4wERow + (16 * j + 4 * fk) * 2) = uint2{l2, h2};
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    // two halves of 16 vectors (register peak): the first half's stores go out before the second
-    // half is read; one barrier after the last image read frees the LDS for the next tile
-    const int om0 = m0, ot0 = t0;
-    const int nwg_next = wg + per_xcd;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      v4u ov[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int qd = lane + 64 * (16 * hf + u), tok = qd >> 4, c16 = qd & 15;
-        ov[u] = *reinterpret_cast<const v4u *>(ew + tok * k4wERow + c16 * 16);
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      if (hf == 1) __syncthreads();        // every wave has its image in registers: the LDS is free
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int qd = lane + 64 * (16 * hf + u), tok = qd >> 4, c16 = qd & 15;
-        const int t = ot0 + 128 * wt + tok, m = om0 + 128 * wm + 8 * c16;
-        if (t < p.T && m < p.M)
-          *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = ov[u];
-      }
-    }
-    if (nwg_next >= xe) break;
-    wg = nwg_next;
-    tile_of(wg, m0, t0);
-    set_offsets(m0, t0);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) { dma_half(0, 0, c, 0); dma_half(0, 0, c, 1); }
-#pragma unroll
-    for (int c = 0; c < 8; ++c) { dma_half(min(1, nsteps - 1), 1, c, 0); dma_half(min(1, nsteps - 1), 1, c, 1); }
-    __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the stores and step 0 have landed
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int g = 0; g < 16; ++g) frag_read(0, 0, g);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // k_gemm16_4p: k_gemm16_4d's step (P1 = 16, P2 = 112, 16x16x32) in a persistent workgroup that
 // walks tiles id, id + grid, ... (grouped XCD-aware order).  The last two steps of a tile stage
 // the NEXT tile's steps 0 and 1, so its k-half 0 fragments are in registers when the tile ends,
@@ -2087,37 +1898,6 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
     hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_BF16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
-  QZ_LAUNCH_CHECK();
-  return QZ_OK;
-}
-
-// measurement twin of qz_gemm_16bit on the persistent epilogue-overlap kernel (k_gemm16_4e)
-extern "C" int qz_gemm_16bit_persistent(int T, int M, int K, const void *X, int ldx, int dtype, const void *W,
-                                        const void *bias, void *Y, int ldy, void *stream) {
-  if (!X || !W || !Y || T < 0 || M < 0 || K < 0) return QZ_ERR_ARG;
-  if (dtype != QZ_DT_F16 && dtype != QZ_DT_BF16) return QZ_ERR_DTYPE;
-  if (T == 0 || M == 0) return QZ_OK;
-  if (!qz_gemm_16bit_ok(T, M, K, X, ldx, W, Y, ldy)) return QZ_ERR_SHAPE;
-  GemmParams p{};
-  p.X = X;
-  p.B = reinterpret_cast<const unsigned char *>(W);
-  p.bias = bias;
-  p.Y = Y;
-  p.T = T;
-  p.M = M;
-  p.K = K;
-  p.ldx = ldx;
-  p.ldy = ldy;
-  p.k_split = K;
-  const int tiles = ((M + k4wM - 1) / k4wM) * ((T + k4wT - 1) / k4wT);
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  int g = std::min(tiles, cus) & ~7;
-  if (g < 8) return QZ_ERR_SHAPE;
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype == QZ_DT_F16) hipLaunchKernelGGL((k_gemm16_4e<QZ_DT_F16>), dim3(g), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((k_gemm16_4e<QZ_DT_BF16>), dim3(g), dim3(256), 0, s, p);
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

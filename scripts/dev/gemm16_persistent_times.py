@@ -1,4 +1,5 @@
-"""Config #4 shapes (T = 16384): qz_gemm_16bit (k_gemm16_4d) vs its persistent epilogue-overlap twin
+"""(Ran against commit 68449ff, which had k_gemm16_4e and qz_gemm_16bit_persistent; both removed after
+the measurement, profiles/r5_gemm16_persistent_times.txt.)  Config #4 shapes (T = 16384): qz_gemm_16bit (k_gemm16_4d) vs its persistent epilogue-overlap twin
 (k_gemm16_4e) vs F.linear (hipBLASLt) on the same fp16 operands; outputs of the two kernels compared."""
 import torch
 import torch.nn.functional as F

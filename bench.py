@@ -217,8 +217,10 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
             from quantizations_amd.parallel import apply_tensor_parallel
             apply_tensor_parallel(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
         else:
-            from quantizations_amd.parallel import shard_model_linear4bit
+            from quantizations_amd.parallel import shard_lm_head, shard_model_linear4bit
             shard_model_linear4bit(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
+            if lm_head:   # the fp16 lm_head's rows too (each rank 1/N of its 1-2 GB), gathered like the rest
+                shard_lm_head(model, rank, world, gatherer=gatherer)
         import gc
         gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
         if torch.cuda.is_available():

@@ -70,6 +70,20 @@ def shard_rows(packed: torch.Tensor, qs: QuantState, rank: int, world: int) -> R
     return RowShard(sub_packed, st, r0, r1, block_base)
 
 
+def gather_rows(y: torch.Tensor, world: int, group=None, gatherer=None) -> torch.Tensor:
+    """Every rank's output rows [..., M/P] -> the full [..., M] on every rank, rank-major."""
+    lead = y.shape[:-1]
+    rows = y.shape[-1]
+    y2 = y.reshape(-1, rows).contiguous()
+    T = y2.shape[0]
+    gathered = torch.empty((world * T, rows), dtype=y.dtype, device=y.device)
+    all_gather_into(gathered, y2, group, gatherer)
+    if T == 1:
+        return gathered.reshape(*lead, world * rows)
+    full = gathered.view(world, T, rows).permute(1, 0, 2).reshape(T, world * rows)
+    return full.reshape(*lead, world * rows)
+
+
 class RowShardedLinear4bit(nn.Module):
     """This rank's rows of a (quantised) ``Linear4bit``; forward returns the FULL
     output on every rank: local fused 4-bit matmul, then an all-gather."""
@@ -116,16 +130,7 @@ class RowShardedLinear4bit(nn.Module):
         all-gather); column-parallel layers (gather=False) and world size 1 return y."""
         if not self.gather or self.world_size == 1:
             return y
-        lead = y.shape[:-1]
-        rows = y.shape[-1]
-        y2 = y.reshape(-1, rows).contiguous()
-        T = y2.shape[0]
-        gathered = torch.empty((self.world_size * T, rows), dtype=y.dtype, device=y.device)
-        all_gather_into(gathered, y2, self.group, self.gatherer)
-        if T == 1:
-            return gathered.reshape(*lead, self.world_size * rows)
-        full = gathered.view(self.world_size, T, rows).permute(1, 0, 2).reshape(T, self.world_size * rows)
-        return full.reshape(*lead, self.world_size * rows)
+        return gather_rows(y, self.world_size, self.group, self.gatherer)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         group = self.__dict__.get("_qz_group")
@@ -408,3 +413,48 @@ def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_s
         else:
             shard_model_linear4bit(child, rank, world_size, group, local_matmul, gatherer)
     return model
+
+
+class RowShardedDenseLinear(nn.Module):
+    """This rank's rows of an unquantised ``nn.Linear`` -- the lm_head, which transformers keeps in
+    the model dtype (128256 rows: 1.05 GB for Llama-3-8B, 2.1 GB for 70B, replicated on every rank
+    otherwise).  forward returns the FULL output on every rank: the local rows (one decode token on
+    the GPU: layer_ops.gemv_dense; anything else F.linear), then the all-gather of the row-split
+    layers.  Each output element is the same dot product as the unsharded layer's."""
+
+    def __init__(self, full: nn.Linear, rank: Optional[int] = None, world_size: Optional[int] = None,
+                 group=None, gatherer=None):
+        super().__init__()
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world_size = dist.get_world_size(group) if world_size is None else world_size
+        self.group, self.gatherer = group, gatherer
+        M = full.out_features
+        if M % self.world_size != 0:
+            raise ValueError(f"out_features {M} is not divisible by world size {self.world_size}")
+        rows = M // self.world_size
+        self.r0, self.r1 = self.rank * rows, (self.rank + 1) * rows
+        self.in_features, self.out_features = full.in_features, M
+        self.register_buffer("weight", full.weight.data[self.r0:self.r1].contiguous().clone(), persistent=False)
+        bias = None if full.bias is None else full.bias.data[self.r0:self.r1].clone()
+        self.register_buffer("bias", bias, persistent=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from .layer_ops import gemv_dense, gemv_dense_supported
+        if self.bias is None and gemv_dense_supported(x, self.weight):
+            y = gemv_dense(x, self.weight)
+        else:
+            y = nn.functional.linear(x, self.weight, self.bias)
+        return y if self.world_size == 1 else gather_rows(y, self.world_size, self.group, self.gatherer)
+
+
+def shard_lm_head(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None, group=None,
+                  gatherer=None) -> bool:
+    """Replace the model's unquantised output projection with this rank's rows of it
+    (RowShardedDenseLinear); False (nothing changed) where it is not an nn.Linear or its rows do
+    not split evenly."""
+    head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
+    world = dist.get_world_size(group) if world_size is None else world_size
+    if not isinstance(head, nn.Linear) or world <= 1 or head.out_features % world != 0:
+        return False
+    model.set_output_embeddings(RowShardedDenseLinear(head, rank, world, group, gatherer))
+    return True

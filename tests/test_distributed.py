@@ -212,7 +212,7 @@ def _tiny_llama_4bit(world: int = 2):
     # world > 2: widths whose column shards keep whole 64-element scale blocks at 8 ranks
     hidden, inter, heads, kv = (128, 256, 4, 2) if world <= 2 else (512, 512, 8, 8)
     cfg = LlamaConfig(hidden_size=hidden, intermediate_size=inter, num_hidden_layers=2, num_attention_heads=heads,
-                      num_key_value_heads=kv, vocab_size=97)
+                      num_key_value_heads=kv, vocab_size=104)   # rows split over 2, 4, 8 ranks (lm_head too)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg).float().eval()
     ref = copy.deepcopy(model)
@@ -351,8 +351,10 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch, layer_ops="none")
         _, ref_hist = bench.decode_bench_graph(ref, cfg, steps=5, warmup=2, prompt_len=6, world=1, batch=batch,
                                                graph=False, device="cpu")
         q_proj = model.model.layers[0].self_attn.q_proj
+        from quantizations_amd.parallel import RowShardedDenseLinear
         q.put((rank, n_groups, bool(torch.equal(hist, ref_hist)), int((hist[:, 6:13] != 0).sum()),
-               isinstance(q_proj, RowShardedLinear4bit) and q_proj.gather))
+               isinstance(q_proj, RowShardedLinear4bit) and q_proj.gather,
+               isinstance(model.get_output_embeddings(), RowShardedDenseLinear)))
     finally:
         dist.destroy_process_group()
 
@@ -366,7 +368,8 @@ def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops, world):
     oracle as each shard's local product: the default strong-scaling layout
     (one bs=1 stream, every Linear4bit row-split + all-gather) and the
     weak-scaling extra (two streams, Megatron pairing).  The greedy tokens of 7
-    decode steps equal the unsharded model's on every rank.  layer_ops "all": the
+    decode steps equal the unsharded model's on every rank (the row split includes the
+    fp16 lm_head: RowShardedDenseLinear).  layer_ops "all": the
     fused decoder layer on the shards (absorbed norms, the sharded SiLU pair, the
     residual epilogues), as bench.py sets it up for N > 1."""
     ctx = mp.get_context("spawn")
@@ -382,11 +385,12 @@ def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops, world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, n_groups, same, n_tok, gathers in res:
+    for rank, n_groups, same, n_tok, gathers, head_rows in res:
         assert n_groups == 4, (rank, n_groups)
         assert same, f"rank {rank}: sharded greedy tokens differ from the unsharded model"
         assert n_tok > 0
         assert gathers == (tp_mode == "gather")
+        assert head_rows == (tp_mode == "gather")   # the fp16 lm_head row-split too
 
 
 def _gemv_hook(x, mod):

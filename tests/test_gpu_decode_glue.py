@@ -234,3 +234,26 @@ def test_llama_decode_dense_lm_head_tokens():
     finally:
         unfuse_layer_ops(model)
     assert torch.equal(hist, ref_hist)
+
+
+def test_row_sharded_lm_head_rows_equal_the_full_launch():
+    """parallel.RowShardedDenseLinear: rank r's local rows of a 128256 x 4096 fp16 lm_head on
+    qz_gemv_dense are bit-identical to rows [r M/N, (r+1) M/N) of the unsharded launch (each row
+    is the same dot product), for N = 2, 4, 8 (the all-gather itself: test_gpu_xgmi_rowsplit.py)."""
+    import torch.nn as nn
+
+    from quantizations_amd.layer_ops import gemv_dense
+    from quantizations_amd.parallel import RowShardedDenseLinear
+
+    M, K = 128256, 4096
+    full = nn.Linear(K, M, bias=False, device=DEV, dtype=torch.float16)
+    with torch.no_grad():
+        full.weight.normal_(0, 0.02)
+    x = torch.randn(1, 1, K, device=DEV).half()
+    ref = gemv_dense(x, full.weight).view(-1)
+    for world in (2, 4, 8):
+        for rank in range(world):
+            mod = RowShardedDenseLinear(full, rank=rank, world_size=world)
+            y = gemv_dense(x, mod.weight).view(-1)
+            assert torch.equal(y, ref[mod.r0:mod.r1])
+            del mod

@@ -61,6 +61,8 @@ def _work(rank, world, port, q, layout):
         ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
         if layout.startswith("gather"):
             shard_model_linear4bit(model, rank, world, gatherer=ag)
+            from quantizations_amd.parallel import shard_lm_head
+            assert shard_lm_head(model, rank, world, gatherer=ag)   # the fp16 lm_head's rows too, as bench.py
         else:   # Megatron pairing: column q/k/v/gate/up, row o/down with the one-shot all-reduce
             apply_tensor_parallel(model, rank, world, gatherer=ag)
         n_groups = fuse_projection_groups(model)

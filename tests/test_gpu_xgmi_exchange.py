@@ -31,9 +31,10 @@ def _worker(rank, world, port, q):
         from quantizations_amd.exchange import OneShotAllGather
 
         dev = torch.device("cuda", 0)
-        ag = OneShotAllGather(slot_bytes=1 << 16, device=dev)
+        ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)   # bench.setup_oneshot's slot
         bad = []
-        sizes = [8, 16, 1024, 7168, 32768, 8, 4096, 14336]     # fp16 elements: 16 B .. 64 KiB
+        # fp16 elements: 16 B .. 64 KiB, and the row-split lm_head's logits (128256 / N rows: N = 2, 8)
+        sizes = [8, 16, 1024, 7168, 32768, 8, 4096, 14336, 64128, 16032]
         for call in range(24):
             n = sizes[call % len(sizes)]
             x = _shard(rank, call, n).to(dev)

@@ -202,8 +202,8 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False,
-                         glue: bool = True, lm_head: bool = True):
+                         mlp_pair: bool = True, mlp_chain: bool = False,
+                         glue: bool = True, lm_head: bool = True, shard_head: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -219,8 +219,9 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
         else:
             from quantizations_amd.parallel import shard_lm_head, shard_model_linear4bit
             shard_model_linear4bit(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
-            if lm_head:   # the fp16 lm_head's rows too (each rank 1/N of its 1-2 GB), gathered like the rest
-                shard_lm_head(model, rank, world, gatherer=gatherer)
+            if shard_head:   # the fp16 lm_head's rows too (each rank 1/N of its 1-2 GB), gathered like the rest
+                shard_lm_head(model, rank, world, gatherer=gatherer,
+                              dense_kernel=lm_head and layer_ops != "none")
         import gc
         gc.collect()  # replaced Linear4bit <-> Params4bit.module cycles hold the full weights until collected
         if torch.cuda.is_available():
@@ -238,8 +239,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
                                      residual=residual, mlp_pair=mlp_pair,
-                                     mlp_chain=mlp_chain,
-                                     qkv_attention=qkv_attention)  # one launch each
+                                     mlp_chain=mlp_chain)  # one launch each
     if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -1158,14 +1158,14 @@ def main():
                          "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
                          "barriers cost more than launch boundaries, DESIGN.md section 12)")
     ap.add_argument("--lm-head-library", action="store_true",
-                    help="keep the fp16 lm_head on F.linear (hipBLASLt) instead of layer_ops.gemv_dense")
+                    help="keep the fp16 lm_head on F.linear (hipBLASLt) instead of layer_ops.gemv_dense (its "
+                         "rows stay split over the ranks; --no-shard-lm-head replicates it)")
+    ap.add_argument("--no-shard-lm-head", action="store_true",
+                    help="N > 1 row-split layout: keep the whole fp16 lm_head on every rank (default: each rank "
+                         "its 1/N of the rows, gathered like the Linear4bit outputs)")
     ap.add_argument("--no-glue", action="store_true",
                     help="keep transformers' own causal-mask and rotary code in the decode step (default: one "
                          "launch each, integration.fuse_decode_glue; same values)")
-    ap.add_argument("--qkv-attention", action="store_true",
-                    help="q/k/v projections and the decode attention as ONE launch (each head's attention in the "
-                         "q/k/v launch's tail, csrc/qkv_attn.hip; measured slower than the default two launches, "
-                         "DESIGN.md section 12)")
     ap.add_argument("--no-residual", action="store_true",
                     help="keep each decoder layer's two residual adds as their own launches (default: in the "
                          "o_proj / down_proj GEMV epilogues)")
@@ -1260,6 +1260,8 @@ def main():
     global GREEDY
     GREEDY = "torch" if args.torch_argmax else args.greedy
 
+    chain_faults = {}
+
     def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int, cdt: torch.dtype = compute_dtype):
         t_build = time.perf_counter()
         model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
@@ -1273,9 +1275,9 @@ def main():
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
                                                      mlp_chain=args.mlp_chain,
-                                                     qkv_attention=args.qkv_attention,
                                                      glue=not args.no_glue,
-                                                     lm_head=not args.lm_head_library)
+                                                     lm_head=not args.lm_head_library,
+                                                     shard_head=not args.no_shard_lm_head)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1288,6 +1290,9 @@ def main():
                 torch.cuda.synchronize()
         if mode == "eager":
             dt, _ = decode_bench(model, cfg, steps, warmup, args.prompt, world, gbatch)
+        if args.mlp_chain:   # a chain that gave up at a grid barrier left untrustworthy outputs: say so
+            from quantizations_amd.integration import mlp_chain_faults
+            chain_faults[tp_mode] = mlp_chain_faults(model, disable=True)
         t = torch.tensor([dt], device="cuda")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time
@@ -1387,11 +1392,11 @@ def main():
         line["config"]["mlp_chain_launch"] = bool(args.mlp_chain and not args.no_residual and not args.no_attention
                                                   and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
                                                   and not sharded)
-        line["config"]["qkv_attention_launch"] = bool(args.qkv_attention and not args.no_attention
-                                                      and not args.no_fuse and layer_ops in ("all", "all+decoder")
-                                                      and not sharded)
+        if args.mlp_chain:
+            line["config"]["mlp_chain_faults"] = chain_faults   # layers whose chain gave up (0 = valid run)
         line["config"]["lm_head"] = "F.linear (hipBLASLt)" if (args.lm_head_library or layer_ops == "none") \
             else "layer_ops.gemv_dense"
+        line["config"]["lm_head_rows_split"] = bool(sharded and tp_mode == "gather" and not args.no_shard_lm_head)
         line["config"]["decode_glue_launches"] = bool(not args.no_glue and layer_ops != "none")
         line["config"]["greedy_argmax"] = {"kernel": "one launch with the feedback (layer_ops.greedy_step)",
                                            "two-stage": "two-stage (greedy_token)", "torch": "torch.argmax"}[GREEDY]

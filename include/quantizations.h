@@ -337,7 +337,8 @@ int qz_decode_attention(int dtype, int B, int Hq, int Hkv, int D, int L, const v
 /* qz_greedy_step: the greedy pick and its feedback (two launches: 2048 logits per workgroup, then
  *   one workgroup over the partials): for b < B, next = argmax_v logits[b*row + v] (v < V;
  *   torch.argmax's order: NaN above every number, the first index among equals),
- *   hist[b*hist_row + *pos] = next, tok[b] = next; then *pos += 1.  int64 hist/pos/tok on the
+ *   hist[b*hist_row + *pos] = next (skipped when *pos is outside [0, hist_len)), tok[b] = next; then
+ *   *pos += 1.  int64 hist/pos/tok on the
  *   device (graph-capturable); F16/BF16/F32 logits; work: qz_greedy_step_work_bytes(B, V) bytes. */
 long long qz_greedy_step_work_bytes(int B, long long V);
 int qz_greedy_step(const void *logits, int dtype, int B, long long V, long long row, long long *hist,
@@ -385,27 +386,9 @@ int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz
                  unsigned *state, void *stream);
 int qz_mlp_chain_state_words(void);
 
-/* A decode token's q/k/v projections AND its attention in ONE launch (round 5, not in the reference;
- * csrc/qkv_attn.hip): qz_gemv_4bit_grouped(_rmsnorm) over segs[0..2] = q_proj, k_proj, v_proj
- * (M = Hq*D, Hkv*D, Hkv*D; their `y` receive q, k, v as before), then qz_decode_attention's rotary,
- * cache update, pos += 1 and masked GQA attention for one sequence (B = 1) over a static cache of
- * L <= 128 positions, out = [Hq*D].  Each query head's attention runs in the q/k/v launch, by the
- * last workgroup that stored the head's rows; the segments' `y` (the q, k, v hand-off) must be
- * UNCACHED device memory (qz_exchange_alloc), or readers may see the previous call's rows.
- * Bit-identical to the two launches.  `state`:
- * qz_qkv_attention_state_words(Hq, Hkv) int32 words, zeroed ONCE and then owned by the calls (one
- * per stream); word (Hq + Hkv + 1) * 32 becomes nonzero if a wait ever gave up.  Shapes the fused
- * launch does not take (L > 128, geometries that split K over waves or put two heads in a
- * workgroup, fp32, unaligned outputs): QZ_ERR_SHAPE, nothing launched -- run the two launches. */
-int qz_gemv_4bit_qkv_attention(const qz_gemv_segment *segs, int K, const void *x, int dtype, int quant_type,
-                               int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,
-                               int Hq, int Hkv, int D, int L, const void *cos, const void *sin, void *k_cache,
-                               void *v_cache, const void *mask, long long mask_j, long long *pos, void *out,
-                               float scale, unsigned *state, void *stream);
-int qz_qkv_attention_state_words(int Hq, int Hkv);
-
 /* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
- * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1: environment variables read ONCE when the library is loaded) and the
+ * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1, and QZ_GEMM16_SCHED -- the k_gemm16_4d schedule qz_gemm_16bit
+ * launches: environment variables read ONCE when the library is loaded) and the
  * device's CU count, as a JSON object written to buf (NUL-terminated when n > the length).
  * Returns the length of the JSON text.  No reference counterpart (measurement bookkeeping). */
 int qz_gemv_knobs(char *buf, int n);

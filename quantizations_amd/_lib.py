@@ -59,9 +59,6 @@ SIGNATURES = {
     "qz_gemv_4bit_residual": [_i, _i, _p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _ll, _p, _p, _p, _p, _p],
     "qz_gemv_4bit_grouped": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p],
     "qz_gemv_4bit_grouped_rmsnorm": [_i, _p, _i, _p, _i, _i, _i, _i, _p, _p, _f, _p],
-    "qz_gemv_4bit_qkv_attention": [_p, _i, _p, _i, _i, _i, _i, _p, _p, _f, _i, _i, _i, _i, _p, _p, _p, _p, _p,
-                                   ctypes.c_longlong, _p, _p, _f, _p, _p],
-    "qz_qkv_attention_state_words": [_i, _i],
     "qz_gemv_4bit_pair_silu": [_p, _i, _p, _i, _i, _i, _i, _p, _p, _f, _p, _p],
     "qz_decode_attention": [_i, _i, _i, _i, _i, _i, _p, _ll, _p, _ll, _p, _ll, _p, _p, _ll, _p, _p, _p, _ll, _ll,
                             _p, _p, _p, _ll, _p, _f, _p],

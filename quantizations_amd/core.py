@@ -501,101 +501,6 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     return h
 
 
-_QKV_SCRATCH = {}
-
-
-def _qkv_scratch(device, nbytes: int) -> int:
-    """Uncached device memory (qz_exchange_alloc: hipDeviceMallocUncached) for the q / k / v rows the
-    fused q/k/v + attention launch hands from its GEMV workgroups to its attention workgroups: with
-    several workgroups per CU, cached lines of the previous call's rows at the same addresses were
-    served to the readers even behind write-through stores and an agent-scope acquire
-    (scripts/dev/qkv_attn_debug4.py); uncached memory has no lines to go stale.  One buffer per
-    device and size, allocated outside any graph capture (the decode warms up eagerly first)."""
-    dev = device.index if device.index is not None else torch.cuda.current_device()
-    key = (dev, int(nbytes))
-    p = _QKV_SCRATCH.get(key)
-    if p is None:
-        vp = ctypes.c_void_p()
-        with torch.cuda.device(dev):
-            check(lib.qz_exchange_alloc(int(nbytes), ctypes.byref(vp)), "qz_exchange_alloc")
-        p = _QKV_SCRATCH[key] = vp.value
-    return p
-
-
-def qkv_attention_state(num_heads: int, num_kv_heads: int, device) -> Tensor:
-    """Counter words of qz_gemv_4bit_qkv_attention (int32, zeroed once; one per stream)."""
-    return torch.zeros(int(lib.qz_qkv_attention_state_words(int(num_heads), int(num_kv_heads))), dtype=torch.int32,
-                       device=device)
-
-
-def gemv_4bit_qkv_attention(x: Tensor, items, norm, cos: Tensor, sin: Tensor, key_cache: Tensor, value_cache: Tensor,
-                            mask: Tensor, pos: Tensor, state: Tensor, num_heads: int, scale: float,
-                            exact_codes: Optional[bool] = None) -> Optional[Tensor]:
-    """A decode token's q/k/v projections (items = [(B, state, bias)] of q_proj, k_proj, v_proj, x the
-    layer input, norm = (weight, eps) of an absorbed input RMSNorm or None) AND its attention
-    against a static cache ([1, Hkv, L, D], L <= 128) in ONE launch (qz_gemv_4bit_qkv_attention):
-    bit-identical to gemv_4bit_grouped(x, items, norm=norm) + layer_ops.decode_attention (cache
-    update and pos += 1 included).  Returns the attention output [1, 1, Hq*D], or None for what the
-    fused launch does not take (the caller runs the two launches)."""
-    if not (x.is_cuda and x.numel() == x.shape[-1] and x.dtype in (torch.float16, torch.bfloat16)):
-        return None
-    if key_cache.dim() != 4 or key_cache.shape[0] != 1 or value_cache.shape != key_cache.shape:
-        return None
-    _, Hkv, L, D = key_cache.shape
-    if L > 128 or D not in (64, 128) or num_heads % Hkv or num_heads // Hkv > 8:
-        return None
-    for t in (key_cache, value_cache):
-        if t.dtype != x.dtype or t.device != x.device or not t.is_contiguous():
-            return None
-    if not (mask.dtype == torch.bool and mask.device == x.device and mask.dim() == 4 and mask.shape[0] == 1
-            and mask.shape[3] == L and cos.shape == sin.shape and cos.dim() == 3 and cos.shape[0] == 1
-            and cos.shape[2] == D and cos.dtype == x.dtype and cos.is_contiguous() and sin.is_contiguous()
-            and pos.dtype == torch.int64 and pos.numel() == 1 and pos.device == x.device):
-        return None
-    items = [tuple(it) for it in items]
-    if len(items) != 3:
-        return None
-    s0 = items[0][1]
-    K = s0.shape[1]
-    if x.shape[-1] != K or [it[1].shape[0] for it in items] != [num_heads * D, Hkv * D, Hkv * D]:
-        return None
-    if any(it[1].shape[1] != K or it[1].quant_type != s0.quant_type or it[1].blocksize != s0.blocksize
-           or it[1].nested != s0.nested or (s0.nested and it[1].state2.blocksize != s0.state2.blocksize)
-           for it in items):
-        return None
-    nw, eps = (None, 0.0) if norm is None else norm
-    if nw is not None and not (nw.dtype == x.dtype and nw.is_cuda and nw.is_contiguous() and nw.numel() == K):
-        return None
-    x = x.contiguous()
-    segs = (_lib.GemvSegment * 3)()
-    rows = [it[1].shape[0] for it in items]
-    base = _qkv_scratch(x.device, 2 * sum(rows))   # q, k, v back to back, 16-bit
-    offs = [0, 2 * rows[0], 2 * (rows[0] + rows[1])]
-    for i, it in enumerate(items):
-        B, st, bias = it[0], it[1], it[2] if len(it) > 2 else None
-        if bias is not None and bias.dtype != x.dtype:
-            bias = bias.to(x.dtype)
-        am, qam, am2, code2, off, _ = st.scale_args()
-        segs[i] = _lib.GemvSegment(st.shape[0], ptr(B), am, qam, am2, code2, off, 0, ptr(bias), base + offs[i])
-    out = torch.empty((1, 1, num_heads * D), dtype=x.dtype, device=x.device)
-    bs2 = int(s0.state2.blocksize) if s0.nested else 0
-    rc = lib.qz_gemv_4bit_qkv_attention(ctypes.cast(segs, ctypes.c_void_p), K, ptr(x), dtype_code(x.dtype),
-                                        _gemv_quant_type(s0.quant_type, exact_codes, x.dtype), s0.blocksize, bs2, 0,
-                                        ptr(nw), float(eps), int(num_heads), int(Hkv), int(D), int(L), ptr(cos),
-                                        ptr(sin), ptr(key_cache), ptr(value_cache), ptr(mask), mask.stride(3),
-                                        ptr(pos), ptr(out), float(scale), ptr(state), _lib.stream_of(x))
-    if rc == _lib.QZ_ERR_SHAPE:
-        return None
-    check(rc, "gemv_4bit_qkv_attention")
-    LAST_FORM["attention"] = "q/k/v + attention (one launch)"
-    return out
-
-
-def qkv_attention_failed(state: Tensor, num_heads: int, num_kv_heads: int) -> bool:
-    """True once a qz_gemv_4bit_qkv_attention call on `state` gave up waiting (synchronises)."""
-    return bool(state[(num_heads + num_kv_heads + 1) * 32].item())
-
-
 def mlp_chain_state(device) -> Tensor:
     """Sync state of qz_mlp_chain (int32 words, zeroed once; one per stream running chains)."""
     return torch.zeros(int(lib.qz_mlp_chain_state_words()), dtype=torch.int32, device=device)

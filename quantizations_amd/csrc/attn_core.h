@@ -1,6 +1,5 @@
-// attn_core.h -- the decode attention of one query head as a device function, shared by the
-// standalone launch (layer_ops.hip: k_decode_attn) and the q/k/v GEMV launch that runs each head's
-// attention in its tail (qkv_attn.hip).
+// attn_core.h -- the decode attention of one query head as a device function over caller-provided
+// LDS (layer_ops.hip: k_decode_attn).
 //
 // Decode attention with a static KV cache (LlamaAttention.forward, modeling_llama.py:243-281, for
 // one new token per sequence): rotary of q and k, the cache update of StaticLayer.update
@@ -22,7 +21,6 @@
 namespace qz {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) unsigned gu32_t;
 
 constexpr int kAttnChunk = 128;  // key positions per workgroup
 // QZ_ATTN_ABL (measurement builds only, scripts/dev/attn_ablation.py; 0 in the product): drop one
@@ -82,13 +80,6 @@ template <int DT> __device__ __forceinline__ float dot2_dt(uint32_t a, uint32_t 
     return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b16x2, a), __builtin_bit_cast(b16x2, b), c, false);
 }
 
-// A 16-bit element of a vector another workgroup of the SAME launch stored write-through (sc1):
-// the 32-bit word holding it, loaded at agent scope (no stale L2 line), then the half
-template <int DT> __device__ __forceinline__ float ld16_agent(const void *base, long long e) {
-  const unsigned w = __hip_atomic_load((const gu32_t *)base + (e >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return from_bits<DT>((e & 1) ? (w >> 16) : w);
-}
-
 // LDS of one head's attention.  `v` is the staged v rows, kAttnChunk x H2 words with the word
 // columns XOR-swizzled by (position & 31): a thread writes its half row at one column across 32
 // consecutive positions per instruction, so an unswizzled 64-word row put every lane of a write
@@ -122,10 +113,8 @@ template <int D> struct AttnLds {
 };
 
 // One query head `hq` of sequence `b` over key chunk `split`, by the 256 threads of the calling
-// workgroup.  SC1: q, k and v were stored write-through by other workgroups of the same launch
-// (qkv_attn.hip) and are loaded at agent scope; otherwise plain loads (a previous launch wrote
-// them).  Returns the position p it read (the caller advances *a.pos once every head is done).
-template <int DT, int D, bool SC1>
+// workgroup (q, k and v come from a previous launch: plain loads).  Returns the position p it read (the caller advances *a.pos once every head is done).
+template <int DT, int D>
 __device__ __forceinline__ long long decode_attn_head(const DecodeAttnArgs &a, int split, int hq, int b,
                                                       const AttnLds<D> &S) {
   constexpr int ES = DT == QZ_DT_F32 ? 4 : 2;
@@ -163,15 +152,9 @@ __device__ __forceinline__ long long decode_attn_head(const DecodeAttnArgs &a, i
     const char *qb = reinterpret_cast<const char *>(a.q) + ((long long)b * a.qs + (long long)hq * D) * ES;
     const char *kb = reinterpret_cast<const char *>(a.k) + ((long long)b * a.ks + (long long)h * D) * ES;
     const char *vb = reinterpret_cast<const char *>(a.v) + ((long long)b * a.vs + (long long)h * D) * ES;
-    if constexpr (SC1) {
-      x1 = ld16_agent<DT>(qb, t); x2 = ld16_agent<DT>(qb, t + H2);
-      k1 = ld16_agent<DT>(kb, t); k2 = ld16_agent<DT>(kb, t + H2);
-      vnew = __hip_atomic_load((const gu32_t *)vb + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      x1 = load_f32<DT>(qb, t); x2 = load_f32<DT>(qb, t + H2);
-      k1 = load_f32<DT>(kb, t); k2 = load_f32<DT>(kb, t + H2);
-      vnew = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
-    }
+    x1 = load_f32<DT>(qb, t); x2 = load_f32<DT>(qb, t + H2);
+    k1 = load_f32<DT>(kb, t); k2 = load_f32<DT>(kb, t + H2);
+    vnew = reinterpret_cast<const uint32_t *>(vb)[t];  // elements 2t, 2t + 1
     c1 = load_f32<DT>(cb, t); c2 = load_f32<DT>(cb, t + H2);
     s1 = load_f32<DT>(sb, t); s2 = load_f32<DT>(sb, t + H2);
   }

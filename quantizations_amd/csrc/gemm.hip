@@ -1234,7 +1234,54 @@ template <int N, typename F> __device__ __forceinline__ void static_for(F &&f) {
 }
 constexpr int k4dBuf = 2 * k4wStage;  // X image + W image of one step
 constexpr int k4dLds = (2 * k4dBuf > 4 * 128 * k4wERow) ? 2 * k4dBuf : 4 * 128 * k4wERow;
-template <int DT, int SK = 0, int P1 = 32, int P2 = 96>
+
+// Split-release step schedule (S = 1): what each wave issues after the c-th of a step's 128
+// MFMAs (16x16x32).  The buffer being read is released per OPERAND: once every wave holds its
+// k-half-1 X fragments the X image takes step s + 2's DMAs, the W image once the W fragments are
+// in; every LDS read has >= 6 MFMAs of cover before the lgkmcnt(0) that precedes a barrier; the
+// one vmcnt wait (13: this step's DMAs issued so far) sits 34 MFMAs before the end, so the 16
+// reads of step s + 1's k-half 0 spread over the rest of the step.  Codes: 1+i read X(k-half 1)
+// i; 9+j read W(k-half 1) j; 17+i read X(next, k-half 0) i; 25+j read W(next) j; 33+c DMA X
+// piece c; 41+c DMA W piece c; 49 lgkmcnt(0) + barrier; 50 vmcnt(13) + barrier.
+struct Gemm4Sched {
+  unsigned char ev[129];
+};
+constexpr Gemm4Sched gemm4_sched_split() {
+  Gemm4Sched t{};
+  const int rx1[8] = {1, 3, 5, 7, 9, 11, 13, 15};
+  const int rw1[8] = {25, 28, 31, 34, 37, 39, 41, 43};
+  const int dx[8] = {23, 26, 29, 32, 35, 53, 56, 59};
+  const int dw[8] = {62, 65, 86, 88, 90, 97, 101, 125};
+  const int rx0[8] = {94, 95, 96, 98, 99, 103, 104, 105};
+  const int rw0[8] = {106, 107, 110, 113, 115, 118, 121, 124};
+  for (int i = 0; i < 8; ++i) {
+    t.ev[rx1[i]] = (unsigned char)(1 + i);
+    t.ev[rw1[i]] = (unsigned char)(9 + i);
+    t.ev[rx0[i]] = (unsigned char)(17 + i);
+    t.ev[rw0[i]] = (unsigned char)(25 + i);
+    t.ev[dx[i]] = (unsigned char)(33 + i);
+    t.ev[dw[i]] = (unsigned char)(41 + i);
+  }
+  t.ev[21] = 49;
+  t.ev[51] = 49;
+  t.ev[92] = 50;
+  return t;
+}
+constexpr Gemm4Sched kGemm4Split = gemm4_sched_split();
+constexpr int gemm4_sched_count(int code) {
+  int n = 0;
+  for (int c = 0; c < 129; ++c) n += kGemm4Split.ev[c] == code;
+  return n;
+}
+constexpr int gemm4_sched_dmas_before(int c0) {
+  int n = 0;
+  for (int c = 0; c < c0; ++c) n += kGemm4Split.ev[c] >= 33 && kGemm4Split.ev[c] < 49;
+  return n;
+}
+static_assert(gemm4_sched_count(0) == 129 - 51, "k_gemm16_4d split schedule: 51 events, one per slot");
+static_assert(gemm4_sched_dmas_before(92) == 13, "k_gemm16_4d split schedule: vmcnt(13) at the wait");
+
+template <int DT, int SK = 0, int P1 = 32, int P2 = 96, int S = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4d(GemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[k4dLds];
   typedef __attribute__((address_space(3))) void *lds_ptr_t;
@@ -1267,12 +1314,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char *>(p.B), (short)0, (int)((uint32_t)p.M * (uint32_t)p.K * 2u), 0x00020000);
   const uint32_t sw = (uint32_t)((tid & 7) ^ ((tid >> 4) & 7));
+  // S & 2: the W image's swizzle is chunk ^ f(row), f = row bits (1, 3, 4) -> chunk bits
+  // (0, 1, 2), the one that keeps the permuted W fragment rows below conflict-free
+  constexpr bool kPerm = (S & 2) != 0;
+  const int wr = tid >> 3;
+  const uint32_t sww = kPerm ? (uint32_t)((tid & 7) ^ (((wr >> 1) & 1) | (((wr >> 3) & 1) << 1) | (((wr >> 4) & 1) << 2)))
+                             : sw;
   uint32_t xo[8], wo[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int row = 32 * c + (tid >> 3);
     xo[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * sw) * 2u;
-    wo[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sw) * 2u;
+    wo[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sww) * 2u;
   }
   // h = 0: X rows, h = 1: W rows
   auto dma_half = [&](int step, int buf, int c, int h) {
@@ -1290,7 +1343,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int fr = lane & 15, fk = lane >> 4;
   const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
                           (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  // S & 2: W fragment j's lane fr reads row 32 (j / 2) + 8 (fr / 4) + 4 (j % 2) + fr % 4 of the
+  // wave's 128 rows, so a lane's accumulators of fragments 2J and 2J + 1 hold 8 CONSECUTIVE
+  // output rows: the epilogue stores them as one 16-B vector straight from the registers.
+  const int fwz = ((fr >> 1) & 1) | (((fr >> 2) & 1) << 1) | (((fr >> 3) & 1) << 2);
+  const uint32_t wl[2] = {(uint32_t)((8 * (fr >> 2) + (fr & 3)) * 128 + ((fk ^ fwz) << 4)),
+                          (uint32_t)((8 * (fr >> 2) + (fr & 3)) * 128 + (((fk ^ fwz) ^ 4) << 4))};
   v4u xf[2][8], wf[2][8];
+  // fragment reads: X tile i / W tile j of k-half kk from buffer buf
+  auto read_x = [&](int buf, int kk, int i) {
+    xf[kk][i] = *reinterpret_cast<const v4u *>(smem + buf * k4dBuf + fl[kk] + (128 * wt + 16 * i) * 128);
+  };
+  auto read_w = [&](int buf, int kk, int j) {
+    const unsigned char *bw = smem + buf * k4dBuf + k4wStage;
+    if constexpr (kPerm)
+      wf[kk][j] = *reinterpret_cast<const v4u *>(bw + wl[kk] + (128 * wm + 32 * (j >> 1) + 4 * (j & 1)) * 128);
+    else
+      wf[kk][j] = *reinterpret_cast<const v4u *>(bw + fl[kk] + (128 * wm + 16 * j) * 128);
+  };
   // SK & 32: v_mfma_f32_32x32x16 (64 MFMAs of 32 cycles per step instead of 128 of 16: half the
   // MFMA issue holds, more issue room for the DMAs and reads).  A/B lane (r32, h32) holds row
   // r32, k = 8 h32 .. +8 of k16 slice 2 kk + q (chunk 2 (2 kk + q) + h32, same swizzle); the 8
@@ -1319,10 +1389,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       return;
     }
-    const unsigned char *bx = bs + fl[kk];
-    const int wj = g == 0 ? 0 : g - 8;
-    if (g >= 1 && g <= 8) xf[kk][g - 1] = *reinterpret_cast<const v4u *>(bx + (128 * wt + 16 * (g - 1)) * 128);
-    else wf[kk][wj] = *reinterpret_cast<const v4u *>(bx + k4wStage + (128 * wm + 16 * wj) * 128);
+    if (g >= 1 && g <= 8) read_x(buf, kk, g - 1);
+    else read_w(buf, kk, g == 0 ? 0 : g - 8);
   };
   f4_t acc[kM32 ? 1 : 8][kM32 ? 1 : 8];
   f16v_t acc32[kM32 ? 4 : 1][kM32 ? 4 : 1];
@@ -1391,13 +1459,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   static_assert(P1 % 16 == 0 && P1 > 0 && P1 <= kNM / 2 && (P2 - P1) % 16 == 0 && P2 > P1 && P2 >= kNM / 2 &&
                 P2 < kNM && (kNM - P2) % 16 == 0, "k_gemm16_4d segment bounds");
   constexpr int kR1 = P1 / 16, kD = (P2 - P1) / 16, kR0 = (kNM - P2) / 16;
+  static_assert(S == 0 || !kM32, "the split-release schedule and the W permutation are written for 16x16x32");
   for (int s = 0; s < nsteps; ++s) {
     const int b = s & 1;
     const int s2 = min(s + 2, nsteps - 1);
     static_for<kNM>([&](auto nc) {
       constexpr int n = decltype(nc)::value;
       mfma(n / (kNM / 2), n % (kNM / 2));
-      if constexpr (n < P1) {
+      if constexpr ((S & 1) != 0) {
+        constexpr int e = kGemm4Split.ev[n + 1];
+        if constexpr (e >= 1 && e <= 8) read_x(b, 1, e - 1);
+        else if constexpr (e >= 9 && e <= 16) read_w(b, 1, e - 9);
+        else if constexpr (e >= 17 && e <= 24) read_x(b ^ 1, 0, e - 17);
+        else if constexpr (e >= 25 && e <= 32) read_w(b ^ 1, 0, e - 25);
+        else if constexpr (e >= 33 && e <= 40) {
+          if constexpr ((SK & 1) == 0) {
+            if (!(S & 4) || s + 2 < nsteps) dma_half(s2, b, e - 33, 0);
+          }
+        } else if constexpr (e >= 41 && e <= 48) {
+          if constexpr ((SK & 1) == 0) {
+            if (!(S & 4) || s + 2 < nsteps) dma_half(s2, b, e - 41, 1);
+          }
+        } else if constexpr (e == 49) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+          __builtin_amdgcn_s_barrier();
+        } else if constexpr (e == 50) {
+          // vmcnt(13): the 13 DMAs this step has issued may stay in flight.  S & 4 (the last
+          // two steps stage nothing): vmcnt(0) there
+          if ((SK & 1) || ((S & 4) && s + 2 >= nsteps)) __builtin_amdgcn_s_waitcnt(0xC07F);
+          else __builtin_amdgcn_s_waitcnt(0x0F7D);
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (e != 0) __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (n < P1) {
         if constexpr ((n + 1) % kR1 == 0) {
           if constexpr ((SK & 2) == 0) frag_read(b, 1, (n + 1) / kR1 - 1);
           __builtin_amdgcn_sched_barrier(0);
@@ -1426,6 +1520,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   if constexpr ((SK & 16) != 0) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+
+  if constexpr (kPerm) {
+    // ---- epilogue straight from the accumulators: fragments 2J, 2J + 1 of token tile i give a
+    // lane 8 consecutive rows of one token -> one 16-B store (16 tokens x 64 B per instruction)
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int m = m0 + 128 * wm + 32 * J + 8 * fk;
+      float bv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bv[r] = p.bias ? load_f32<DT>(p.bias, min(m + r, p.M - 1)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = t0 + 128 * wt + 16 * i + fr;
+        const f4_t lo = acc[2 * J][i], hi = acc[2 * J + 1][i];
+        const v4u o = v4u{cvt_pk16<DT>(lo[0] + bv[0], lo[1] + bv[1]), cvt_pk16<DT>(lo[2] + bv[2], lo[3] + bv[3]),
+                          cvt_pk16<DT>(hi[0] + bv[4], hi[1] + bv[5]), cvt_pk16<DT>(hi[2] + bv[6], hi[3] + bv[7])};
+        if constexpr ((SK & 128) != 0) {  // timing only: no global stores
+          if (o.x == 0x7FFF7FFFu && o.y == 0x12345678u) *reinterpret_cast<v4u *>(p.Y) = o;
+          continue;
+        }
+        if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = o;
+      }
+    }
+    return;
+  }
 
   // ---- epilogue: quadrant -> LDS image [128 tokens][128 rows] (+ bias) -> coalesced rows ----
   __syncthreads();
@@ -1870,6 +1989,13 @@ using namespace qz;
 
 static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0; }
 
+// QZ_GEMM16_SCHED (read once at load, reported and set through qz_gemv_knobs / qz_gemv_set_knob):
+// the k_gemm16_4d schedule qz_gemm_16bit launches -- 0: P1/P2 segments; S bits: 1 split-release
+// schedule, 2 permuted W rows + 16-B register epilogue, 4 no staging in the last two steps
+namespace qz {
+int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
+}
+
 extern "C" int qz_gemm_16bit_ok(int T, int M, int K, const void *X, int ldx, const void *W, const void *Y, int ldy);
 
 // Dense 16-bit GEMM (k_gemm16_4d: 4 waves, 256 x 256 tile, LDS-DMA staging two steps ahead): the
@@ -1894,10 +2020,22 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   p.k_split = K;
   const unsigned g = (unsigned)(((M + k4wM - 1) / k4wM) * ((T + k4wT - 1) / k4wT));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == QZ_DT_F16)
-    hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_BF16, 64, 16, 112>), dim3(g), dim3(256), 0, s, p);
+#define QZ_G16(DT_, S_) hipLaunchKernelGGL((k_gemm16_4d<DT_, 64, 16, 112, S_>), dim3(g), dim3(256), 0, s, p)
+#define QZ_G16S(DT_)                   \
+  switch (gemm16_sched()) {            \
+    case 1: QZ_G16(DT_, 1); break;     \
+    case 2: QZ_G16(DT_, 2); break;     \
+    case 3: QZ_G16(DT_, 3); break;     \
+    case 7: QZ_G16(DT_, 7); break;     \
+    default: QZ_G16(DT_, 0); break;    \
+  }
+  if (dtype == QZ_DT_F16) {
+    QZ_G16S(QZ_DT_F16)
+  } else {
+    QZ_G16S(QZ_DT_BF16)
+  }
+#undef QZ_G16S
+#undef QZ_G16
   QZ_LAUNCH_CHECK();
   return QZ_OK;
 }

@@ -61,6 +61,9 @@ static Knobs read_knobs() {
 }
 static Knobs g_knobs = read_knobs();   // at library load
 Knobs &gemv_knobs() { return g_knobs; }
+// QZ_GEMM16_SCHED: the k_gemm16_4d schedule qz_gemm_16bit launches (gemm.hip)
+static int g_gemm16_sched = env_int("QZ_GEMM16_SCHED", 0);
+int &gemm16_sched() { return g_gemm16_sched; }
 
 template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, bool TWO, int STAMP = 0>
 __global__ __launch_bounds__(NW * 64) void k_gemv_4bit(GemvParams p) {
@@ -511,12 +514,12 @@ extern "C" int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const 
 // The launch-geometry knobs in effect (read once at library load) as a JSON object, for the bench
 // line's config.  Returns the length written (excluding the NUL), or the length needed if n is too small.
 extern "C" int qz_gemv_knobs(char *buf, int n) {
-  char tmp[256];
+  char tmp[320];
   const int len = snprintf(tmp, sizeof(tmp),
                            "{\"QZ_GEMV_WIDE8\": %d, \"QZ_GROUPED_NORM_R\": %d, \"QZ_PAIR_R\": %d, \"QZ_PAIR_WT\": %d, "
-                           "\"QZ_PAIR_PS\": %d, \"QZ_PAIR_WK1\": %d, \"cus\": %d}",
+                           "\"QZ_PAIR_PS\": %d, \"QZ_PAIR_WK1\": %d, \"QZ_GEMM16_SCHED\": %d, \"cus\": %d}",
                            gemv_knobs().wide8, gemv_knobs().norm_r, gemv_knobs().pair_r, gemv_knobs().pair_wt,
-                           gemv_knobs().pair_ps, gemv_knobs().pair_wk1, device_cus());
+                           gemv_knobs().pair_ps, gemv_knobs().pair_wk1, gemm16_sched(), device_cus());
   if (buf && n > len) memcpy(buf, tmp, (size_t)len + 1);
   return len;
 }
@@ -532,6 +535,7 @@ extern "C" int qz_gemv_set_knob(const char *name, int value) {
   else if (!strcmp(name, "QZ_PAIR_WT")) k.pair_wt = value != 0;
   else if (!strcmp(name, "QZ_PAIR_PS")) k.pair_ps = value;
   else if (!strcmp(name, "QZ_PAIR_WK1")) k.pair_wk1 = value;
+  else if (!strcmp(name, "QZ_GEMM16_SCHED")) gemm16_sched() = value;
   else return QZ_ERR_ARG;
   return QZ_OK;
 }

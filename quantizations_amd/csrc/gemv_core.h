@@ -586,20 +586,9 @@ struct GemvGroup {
 //  workgroups -- each takes row blocks blockIdx.x, + gridDim.x, ..., so its prologue (byte table,
 //  code2, the normalised x) is paid once, and the next block's first step is issued before the
 //  current block's epilogue.
-// TailT: work the workgroup does after its rows are stored (qkv_attn.hip: each query head's
-// attention, by the last workgroup to store that head's rows).  kSc1: the output stores go
-// write-through (agent-scope relaxed atomic stores) so other workgroups of the launch may read them;
-// the tail gets the byte table's LDS (32 KiB) and the dynamic image region once every wave is done.
-struct NoTail {
-  static constexpr bool kActive = false;
-  __device__ void operator()(unsigned char *, unsigned char *) const {}
-};
 template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, bool NRM, bool PAIR, bool TWO, bool PS,
-          int STAMP = 0, class TailT = NoTail>
-__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block, const GemvParams *pair = nullptr,
-                                          const TailT &tail = TailT{}) {
-  static_assert(!TailT::kActive || (WK == 1 && !PAIR && !PS && !WT && NW == 4 && DT != QZ_DT_F32 && R % 2 == 0),
-                "tail: whole rows per wave, 4 waves, packed 16-bit row-pair stores, the 32 KiB table");
+          int STAMP = 0>
+__device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int block, const GemvParams *pair = nullptr) {
   static_assert(!NRM || (NW == 4 && FS && DT != QZ_DT_F32), "fused pre-norm: 4 waves, full steps, 16-bit activations");
   static_assert(!PAIR || (NW == 4 && WK == 1 && DT != QZ_DT_F32), "pair: 4 waves, WK = 1, 16-bit activations");
   static_assert(!PS || (PAIR && FS), "persistent form: pair launches, full steps");
@@ -928,11 +917,7 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
           }
           o0 = add_res<DT>(o0, p.res, row0 + r);
           o1 = add_res<DT>(o1, p.res, row0 + r + 1);
-          if constexpr (TailT::kActive)
-            __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)p.y + ((row0 + r) >> 1), pack16<DT>(o0, o1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            reinterpret_cast<uint32_t *>(p.y)[(row0 + r) >> 1] = pack16<DT>(o0, o1);
+          reinterpret_cast<uint32_t *>(p.y)[(row0 + r) >> 1] = pack16<DT>(o0, o1);
         }
       } else {
 #pragma unroll
@@ -949,7 +934,6 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
     }
     QZ_STAMP(4);
     QZ_STAMP_FLUSH(block * NW + wave);
-    if constexpr (TailT::kActive) tail(reinterpret_cast<unsigned char *>(s_tab), s_x);
     return;
   }
 #pragma unroll

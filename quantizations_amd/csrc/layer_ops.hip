@@ -224,14 +224,14 @@ __global__ __launch_bounds__(256) void k_silu_mul_vec(const void *__restrict__ g
 }
 
 // ---------------------------------------------------------------------------
-// Decode attention with a static KV cache: one query head per workgroup, the body in attn_core.h
-// (shared with the q/k/v launch that runs it in its tail, qkv_attn.hip).  Grid (nsplit, Hq, B).
+// Decode attention with a static KV cache: one query head per workgroup, the body in attn_core.h.
+// Grid (nsplit, Hq, B).
 template <int DT, int D>
 __global__ __launch_bounds__(256) void k_decode_attn(DecodeAttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_v[kAttnChunk * (D / 2)];
   __shared__ __attribute__((aligned(16))) unsigned char s_small[AttnLds<D>::kSmallBytes];
   const AttnLds<D> S{s_v, s_small};
-  const long long p = decode_attn_head<DT, D, false>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
+  const long long p = decode_attn_head<DT, D>(a, blockIdx.x, blockIdx.y, blockIdx.z, S);
   // the last workgroup to arrive advances the cache position (every workgroup has read p)
   __syncthreads();
   if (threadIdx.x == 0 && (kAttnAbl & 1) == 0) {
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256) void k_greedy_partial(const void *logits, long
 }
 __global__ __launch_bounds__(256) void k_greedy_final(int B, long long V, int nb, const float *pv,
                                                       const long long *pi, long long *hist, long long hist_row,
-                                                      long long *pos, long long *tok) {
+                                                      long long hist_len, long long *pos, long long *tok) {
   __shared__ float s_v[4];
   __shared__ long long s_i[4];
   const int tid = threadIdx.x;
@@ -452,7 +452,9 @@ __global__ __launch_bounds__(256) void k_greedy_final(int B, long long V, int nb
     }
     greedy_reduce_wg(best, bi, V, s_v, s_i);
     if (tid == 0) {
-      hist[(size_t)b * hist_row + p] = bi;
+      // a position past the history (a graph replayed more often than hist has columns) writes
+      // nothing there: the token and the position still advance
+      if (p >= 0 && p < hist_len) hist[(size_t)b * hist_row + p] = bi;
       tok[b] = bi;
     }
   }
@@ -677,7 +679,7 @@ extern "C" int qz_greedy_step(const void *logits, int dtype, int B, long long V,
     case QZ_DT_F32: hipLaunchKernelGGL((k_greedy_partial<QZ_DT_F32>), g, dim3(256), 0, s, logits, row, V, nb, pv, pi, vec); break;
     default: return QZ_ERR_DTYPE;
   }
-  hipLaunchKernelGGL(k_greedy_final, dim3(1), dim3(256), 0, s, B, V, nb, pv, pi, hist, hist_row, pos, tok);
+  hipLaunchKernelGGL(k_greedy_final, dim3(1), dim3(256), 0, s, B, V, nb, pv, pi, hist, hist_row, hist_len, pos, tok);
   return (int)hipGetLastError();
 }
 

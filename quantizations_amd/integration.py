@@ -296,6 +296,25 @@ def _mlp_chain(layer: nn.Module, x: torch.Tensor, residual: torch.Tensor):
     return gemv_4bit_mlp_chain(x, residual, item(o), item(g), item(u), item(d), grp.prenorm[:2], st, exact_codes=ex)
 
 
+def mlp_chain_faults(model: nn.Module, disable: bool = True) -> int:
+    """How many layers' persistent MLP chains (fuse_layer_ops(mlp_chain=True)) ever gave up waiting at a
+    grid barrier (core.mlp_chain_failed: the launch then ends with outputs that cannot be trusted).
+    Synchronises.  With `disable`, a fault turns the chain off in every layer (the three launches run
+    from then on); callers check after a warm-up and again after a timed run."""
+    from .core import mlp_chain_failed
+
+    bad = 0
+    layers = [m for m in model.modules() if "_qz_mlp_chain" in m.__dict__]
+    for m in layers:
+        st = m.__dict__.get("_qz_chain_state")
+        if st is not None and mlp_chain_failed(st):
+            bad += 1
+    if bad and disable:
+        for m in layers:
+            m.__dict__["_qz_mlp_chain"] = False
+    return bad
+
+
 def _residual_decoder_forward(mod: nn.Module):
     """LlamaDecoderLayer.forward (modeling_llama.py:295-324) with both `residual + h` adds
     moved into the epilogues of the o_proj and down_proj GEMVs (their modules were patched by
@@ -366,11 +385,6 @@ def _fused_attention_forward(mod: nn.Module, orig):
                 if arrive is None or arrive.device != hidden_states.device:
                     arrive = torch.zeros(1, dtype=torch.int32, device=hidden_states.device)
                     mod.__dict__["_qz_attn_arrive"] = arrive
-                out = _qkv_attention(mod, hidden_states, cos, sin, layer, attention_mask, nq)
-                if out is not None:   # q/k/v and the attention in one launch
-                    if _qz_o_tail is not None and _qz_residual is not None:
-                        return _qz_o_tail(out, _qz_residual), None
-                    return _project(mod.o_proj, out, _qz_residual), None
                 q = mod.q_proj(hidden_states)
                 k = mod.k_proj(hidden_states)
                 v = mod.v_proj(hidden_states)
@@ -385,45 +399,6 @@ def _fused_attention_forward(mod: nn.Module, orig):
         h, w = orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
         return (h if _qz_residual is None else _qz_residual + h), w
     return forward
-
-
-def _qkv_attention(mod: nn.Module, x: torch.Tensor, cos, sin, layer, mask, nq: int):
-    """The attention module's q/k/v projections and its decode attention as ONE launch
-    (core.gemv_4bit_qkv_attention; bit-identical to the grouped launch + decode_attention), or None
-    where it does not apply: q/k/v must be plain Linear4bit layers forming one decode group (its
-    absorbed input norm, if any, rides along), one sequence of one token, a static cache of at most
-    128 positions, and fuse_layer_ops(qkv_attention=True)."""
-    from .core import exact_codes_for, gemv_4bit_qkv_attention, qkv_attention_state
-
-    if not mod.__dict__.get("_qz_qkv_attn"):
-        return None
-    qp, kp, vp = mod.q_proj, mod.k_proj, mod.v_proj
-    if any(type(m) is not Linear4bit or m.weight.quant_state is None for m in (qp, kp, vp)):
-        return None
-    grp = qp.__dict__.get("_qz_group")
-    if grp is None or grp._compute is not _linear4bit_group_compute or \
-            [id(m) for m in grp.members] != [id(qp), id(kp), id(vp)]:
-        return None
-    if x.shape[0] != 1 or x.numel() != x.shape[-1] or layer.keys.shape[0] != 1:
-        return None
-    for m in (qp, kp, vp):
-        if not m.compute_type_is_set:
-            m.set_compute_type(x)
-            m.compute_type_is_set = True
-        if m._input(x) is not x:
-            return None
-    ex = exact_codes_for(qp.compute_dtype)
-    if any(exact_codes_for(m.compute_dtype) != ex for m in (kp, vp)):
-        return None
-    Hkv = layer.keys.shape[1]
-    st = mod.__dict__.get("_qz_qkv_state")
-    if st is None or st.device != x.device:
-        st = qkv_attention_state(nq, Hkv, x.device)
-        mod.__dict__["_qz_qkv_state"] = st
-    items = [(m.weight, m.weight.quant_state, None if m.bias is None else m.bias.to(x.dtype)) for m in (qp, kp, vp)]
-    norm = grp.prenorm[:2] if grp.prenorm is not None else None
-    return gemv_4bit_qkv_attention(x, items, norm, cos, sin, layer.keys, layer.values, mask, layer.cumulative_length,
-                                   st, nq, mod.scaling, exact_codes=ex)
 
 
 def _project(proj: nn.Module, x: torch.Tensor, residual):
@@ -461,7 +436,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
                    decoder: bool = False, attention: bool = True, residual: bool = True,
-                   mlp_pair: bool = True, mlp_chain: bool = False, qkv_attention: bool = False) -> int:
+                   mlp_pair: bool = True, mlp_chain: bool = False) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -480,11 +455,7 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     with `residual`) lets a residual-fused decoder layer run a decode token's o_proj + residual,
     post-attention norm, MLP and second residual as ONE persistent launch (_mlp_chain) where the
     layer qualifies (after fuse_prenorm): bit-identical, but measured slower than the three launches
-    (each in-kernel grid barrier costs 6-7 us against a ~1.5 us launch boundary).
-    `qkv_attention` (opt-in, with `attention`) lets a decode token's q/k/v projections and attention
-    run as ONE launch where the projections form a plain Linear4bit decode group (_qkv_attention):
-    bit-identical, but measured slower than the two launches (Llama-3-8B decode 577 vs 590 tok/s on
-    one box)."""
+    (each in-kernel grid barrier costs 6-7 us against a ~1.5 us launch boundary)."""
     import sys
 
     n = 0
@@ -511,7 +482,6 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
                     hasattr(m, a) for a in ("q_proj", "k_proj", "v_proj", "o_proj", "scaling", "head_dim")):
                 m.__dict__["forward"] = _fused_attention_forward(m, m.forward)
                 m.__dict__["_qz_fused_attn"] = True
-                m.__dict__["_qz_qkv_attn"] = bool(qkv_attention)
                 n += 1
             if not rope:
                 continue
@@ -548,8 +518,6 @@ def unfuse_layer_ops(model: nn.Module) -> None:
             m.__dict__.pop("_qz_attn_arrive", None)
             m.__dict__.pop("_qz_mlp_chain", None)
             m.__dict__.pop("_qz_chain_state", None)
-            m.__dict__.pop("_qz_qkv_attn", None)
-            m.__dict__.pop("_qz_qkv_state", None)
     for modname, fn in list(_ROPE_PATCHED.items()):
         setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)
         del _ROPE_PATCHED[modname]

@@ -420,11 +420,13 @@ class RowShardedDenseLinear(nn.Module):
     the model dtype (128256 rows: 1.05 GB for Llama-3-8B, 2.1 GB for 70B, replicated on every rank
     otherwise).  forward returns the FULL output on every rank: the local rows (one decode token on
     the GPU: layer_ops.gemv_dense; anything else F.linear), then the all-gather of the row-split
-    layers.  Each output element is the same dot product as the unsharded layer's."""
+    layers.  Each output element is the same dot product as the unsharded layer's.  `dense_kernel`
+    False keeps F.linear for the local rows too (the bench's --lm-head-library)."""
 
     def __init__(self, full: nn.Linear, rank: Optional[int] = None, world_size: Optional[int] = None,
-                 group=None, gatherer=None):
+                 group=None, gatherer=None, dense_kernel: bool = True):
         super().__init__()
+        self.dense_kernel = dense_kernel
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world_size = dist.get_world_size(group) if world_size is None else world_size
         self.group, self.gatherer = group, gatherer
@@ -440,7 +442,7 @@ class RowShardedDenseLinear(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from .layer_ops import gemv_dense, gemv_dense_supported
-        if self.bias is None and gemv_dense_supported(x, self.weight):
+        if self.dense_kernel and self.bias is None and gemv_dense_supported(x, self.weight):
             y = gemv_dense(x, self.weight)
         else:
             y = nn.functional.linear(x, self.weight, self.bias)
@@ -448,13 +450,19 @@ class RowShardedDenseLinear(nn.Module):
 
 
 def shard_lm_head(model: nn.Module, rank: Optional[int] = None, world_size: Optional[int] = None, group=None,
-                  gatherer=None) -> bool:
+                  gatherer=None, dense_kernel: bool = True) -> bool:
     """Replace the model's unquantised output projection with this rank's rows of it
-    (RowShardedDenseLinear); False (nothing changed) where it is not an nn.Linear or its rows do
-    not split evenly."""
+    (RowShardedDenseLinear); False (nothing changed) where it is not an nn.Linear, its rows do
+    not split evenly, or it is tied to the input embedding (tie_word_embeddings: the embedding
+    stays whole, so nothing would be saved, and a later model.tie_weights() would put the full
+    embedding Parameter back in place of the rank's rows)."""
     head = model.get_output_embeddings() if hasattr(model, "get_output_embeddings") else None
     world = dist.get_world_size(group) if world_size is None else world_size
     if not isinstance(head, nn.Linear) or world <= 1 or head.out_features % world != 0:
         return False
-    model.set_output_embeddings(RowShardedDenseLinear(head, rank, world, group, gatherer))
+    emb = model.get_input_embeddings() if hasattr(model, "get_input_embeddings") else None
+    if getattr(getattr(model, "config", None), "tie_word_embeddings", False) or \
+            (emb is not None and getattr(emb, "weight", None) is head.weight):
+        return False
+    model.set_output_embeddings(RowShardedDenseLinear(head, rank, world, group, gatherer, dense_kernel))
     return True

@@ -173,6 +173,25 @@ def test_greedy_step_is_torch_argmax_and_feedback(dtype, B, V):
         assert torch.equal(hist, hist_r) and torch.equal(pos, pos_r)
 
 
+@pytest.mark.parametrize("B", [1, 2])
+def test_greedy_step_position_past_history(B):
+    """pos == H (a graph replayed once more than hist has columns): nothing is written at column H
+    -- the next row's first entry, or the guard words after the last row -- while tok and pos still
+    advance."""
+    from quantizations_amd.layer_ops import greedy_step
+
+    H, V = 8, 1000
+    logits = torch.randn(B, V, device=DEV, generator=torch.Generator(device="cuda").manual_seed(B))
+    flat = torch.full((B * H + 4,), -7, dtype=torch.int64, device=DEV)
+    hist = flat[:B * H].view(B, H)
+    pos = torch.tensor([H], device=DEV)
+    tok = torch.zeros(B, dtype=torch.int64, device=DEV)
+    greedy_step(logits, hist, pos, tok)
+    torch.cuda.synchronize()
+    assert bool((flat == -7).all())
+    assert torch.equal(tok, logits.argmax(-1)) and int(pos.item()) == H + 1
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("M,K", [(5000, 4096), (4099, 8192), (17, 4096), (1, 8192)])
 def test_gemv_dense_against_fp64_and_library(dtype, M, K):

@@ -203,7 +203,8 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
                          mlp_pair: bool = True, mlp_chain: bool = False,
-                         glue: bool = True, lm_head: bool = True, shard_head: bool = True):
+                         glue: bool = True, lm_head: bool = True, shard_head: bool = True,
+                         head_sharded_attention: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
     Linear4bit for the multi-GPU layout (tp_mode "gather": row split + all-gather,
     "pair": Megatron column/row pairing), attach the q/k/v and gate/up decode
@@ -217,8 +218,10 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
             from quantizations_amd.parallel import apply_tensor_parallel
             apply_tensor_parallel(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
         else:
-            from quantizations_amd.parallel import shard_lm_head, shard_model_linear4bit
+            from quantizations_amd.parallel import shard_attention_heads, shard_lm_head, shard_model_linear4bit
             shard_model_linear4bit(model, rank, world, local_matmul=local_matmul, gatherer=gatherer)
+            if head_sharded_attention:   # q/k/v rows stay local: each rank attends over its own heads
+                shard_attention_heads(model)
             if shard_head:   # the fp16 lm_head's rows too (each rank 1/N of its 1-2 GB), gathered like the rest
                 shard_lm_head(model, rank, world, gatherer=gatherer,
                               dense_kernel=lm_head and layer_ops != "none")
@@ -1160,6 +1163,10 @@ def main():
     ap.add_argument("--lm-head-library", action="store_true",
                     help="keep the fp16 lm_head on F.linear (hipBLASLt) instead of layer_ops.gemv_dense (its "
                          "rows stay split over the ranks; --no-shard-lm-head replicates it)")
+    ap.add_argument("--replicated-attention", action="store_true",
+                    help="N > 1 row-split layout: gather q/k/v and run every head's attention on every rank "
+                         "(default: head-sharded -- each rank's q/k/v rows are whole heads, attended locally, "
+                         "and the attention output is gathered before o_proj)")
     ap.add_argument("--no-shard-lm-head", action="store_true",
                     help="N > 1 row-split layout: keep the whole fp16 lm_head on every rank (default: each rank "
                          "its 1/N of the rows, gathered like the Linear4bit outputs)")
@@ -1277,7 +1284,8 @@ def main():
                                                      mlp_chain=args.mlp_chain,
                                                      glue=not args.no_glue,
                                                      lm_head=not args.lm_head_library,
-                                                     shard_head=not args.no_shard_lm_head)
+                                                     shard_head=not args.no_shard_lm_head,
+                                                     head_sharded_attention=not args.replicated_attention)
         log(f"[rank {rank}] model ready in {time.perf_counter() - t_build:.1f}s, "
             f"{torch.cuda.memory_allocated() / 2**30:.2f} GiB ({tp_mode if sharded else 'single'}, batch {gbatch})")
         mode = "eager"
@@ -1397,6 +1405,10 @@ def main():
         line["config"]["lm_head"] = "F.linear (hipBLASLt)" if (args.lm_head_library or layer_ops == "none") \
             else "layer_ops.gemv_dense"
         line["config"]["lm_head_rows_split"] = bool(sharded and tp_mode == "gather" and not args.no_shard_lm_head)
+        line["config"]["attention"] = ("head-sharded (local q/k/v heads, attention output gathered)"
+                                       if sharded and tp_mode == "gather" and not args.replicated_attention
+                                       else "replicated" if sharded and tp_mode == "gather" else
+                                       "local heads (TP pairing)" if sharded else "single GPU")
         line["config"]["decode_glue_launches"] = bool(not args.no_glue and layer_ops != "none")
         line["config"]["greedy_argmax"] = {"kernel": "one launch with the feedback (layer_ops.greedy_step)",
                                            "two-stage": "two-stage (greedy_token)", "torch": "torch.argmax"}[GREEDY]

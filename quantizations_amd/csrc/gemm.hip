@@ -1268,6 +1268,22 @@ constexpr Gemm4Sched gemm4_sched_split() {
   return t;
 }
 constexpr Gemm4Sched kGemm4Split = gemm4_sched_split();
+// The same schedule with every read / DMA one MFMA later where that slot is free (the waits stay):
+// S & 16 gives it to the waves on odd SIMDs, so the two SIMD pairs do not hit the LDS and the
+// address path in the same cycles
+constexpr Gemm4Sched gemm4_sched_shift(Gemm4Sched a) {
+  Gemm4Sched t{};
+  for (int c = 128; c >= 1; --c) {
+    const int e = a.ev[c];
+    if (e == 0) continue;
+    if (e < 49 && c + 1 <= 128 && a.ev[c + 1] == 0 && t.ev[c + 1] == 0 && c + 1 != 92 && c + 1 != 21 && c + 1 != 51)
+      t.ev[c + 1] = (unsigned char)e;
+    else
+      t.ev[c] = (unsigned char)e;
+  }
+  return t;
+}
+constexpr Gemm4Sched kGemm4SplitB = gemm4_sched_shift(kGemm4Split);
 constexpr int gemm4_sched_count(int code) {
   int n = 0;
   for (int c = 0; c < 129; ++c) n += kGemm4Split.ev[c] == code;
@@ -1279,8 +1295,33 @@ constexpr int gemm4_sched_dmas_before(int c0) {
   return n;
 }
 static_assert(gemm4_sched_count(0) == 129 - 51, "k_gemm16_4d split schedule: 51 events, one per slot");
+constexpr int gemm4_sched_b_count(int code) {
+  int n = 0;
+  for (int c = 0; c < 129; ++c) n += kGemm4SplitB.ev[c] == code;
+  return n;
+}
+constexpr int gemm4_sched_b_dmas_before(int c0) {
+  int n = 0;
+  for (int c = 0; c < c0; ++c) n += kGemm4SplitB.ev[c] >= 33 && kGemm4SplitB.ev[c] < 49;
+  return n;
+}
+static_assert(gemm4_sched_b_count(0) == 129 - 51 && kGemm4SplitB.ev[128] == 0, "shifted schedule: 51 events");
+static_assert(gemm4_sched_b_dmas_before(92) == 13 && kGemm4SplitB.ev[21] == 49 && kGemm4SplitB.ev[51] == 49 &&
+              kGemm4SplitB.ev[92] == 50, "shifted schedule: the waits unchanged");
 static_assert(gemm4_sched_dmas_before(92) == 13, "k_gemm16_4d split schedule: vmcnt(13) at the wait");
 
+// QZ_STAMPS_G16 (microbenchmark builds only): s_memtime of each wave of workgroups 0-7 at the
+// kernel start, after the prologue barrier, around the waits of step kStampStep, the loop end and
+// the epilogue end -- where a step's cycles go
+#ifdef QZ_STAMPS_G16
+__device__ unsigned long long g_qz_stamp_g16[8 * 4 * 16];
+constexpr int kStampStep = 20;
+#define QZ_G16_STAMP(k) do { if (blockIdx.x < 8) g_qz_stamp_g16[(blockIdx.x * 4 + wave) * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define QZ_G16_STAMP_AT(k, st) do { if ((st) == kStampStep) QZ_G16_STAMP(k); } while (0)
+#else
+#define QZ_G16_STAMP(k) do { } while (0)
+#define QZ_G16_STAMP_AT(k, st) do { } while (0)
+#endif
 template <int DT, int SK = 0, int P1 = 32, int P2 = 96, int S = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4d(GemmParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[k4dLds];
@@ -1288,6 +1329,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wt = wave >> 1, wm = wave & 1;
+  QZ_G16_STAMP(0);
+  QZ_G16_STAMP(0);
 
   // XCD-aware, bijective tile order (as k_gemm_4bit_big)
   const int tiles_m = (p.M + k4wM - 1) / k4wM;
@@ -1444,6 +1487,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int c = 0; c < 8; ++c) dma(min(1, nsteps - 1), 1, c);
   __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
   __builtin_amdgcn_s_barrier();
+  QZ_G16_STAMP(1);
 #pragma unroll
   for (int g = 0; g < 16; ++g) frag_read(0, 0, g);
   if constexpr ((SK & 16) != 0) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -1460,45 +1504,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 P2 < kNM && (kNM - P2) % 16 == 0, "k_gemm16_4d segment bounds");
   constexpr int kR1 = P1 / 16, kD = (P2 - P1) / 16, kR0 = (kNM - P2) / 16;
   static_assert(S == 0 || !kM32, "the split-release schedule and the W permutation are written for 16x16x32");
+  static_assert((S & 8) == 0 || (S & 1) != 0, "the rotated loop is the split-release schedule's");
+  // MFMA n of step s (buffer s & 1) and the event the split-release table puts after it, every
+  // MFMA pinned in program order
+  auto split_mfma = [&](auto nc, int s, auto tb) {
+    constexpr int n = decltype(nc)::value;
+    constexpr bool kB = decltype(tb)::value;
+    const int b = s & 1;
+    const int s2 = min(s + 2, nsteps - 1);
+    if constexpr (n == 0) QZ_G16_STAMP_AT(2, s);
+    if constexpr (n == 0) QZ_G16_STAMP_AT(9, s - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma(n / 64, n % 64);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int e = kB ? kGemm4SplitB.ev[n + 1] : kGemm4Split.ev[n + 1];
+    if constexpr (e >= 1 && e <= 8) read_x(b, 1, e - 1);
+    else if constexpr (e >= 9 && e <= 16) read_w(b, 1, e - 9);
+    else if constexpr (e >= 17 && e <= 24) read_x(b ^ 1, 0, e - 17);
+    else if constexpr (e >= 25 && e <= 32) read_w(b ^ 1, 0, e - 25);
+    else if constexpr (e >= 33 && e <= 40) {
+      if constexpr ((SK & 1) == 0) dma_half(s2, b, e - 33, 0);
+    } else if constexpr (e >= 41 && e <= 48) {
+      if constexpr ((SK & 1) == 0) dma_half(s2, b, e - 41, 1);
+    } else if constexpr (e == 49) {
+      QZ_G16_STAMP_AT(n < 40 ? 3 : 5, s);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      QZ_G16_STAMP_AT(n < 40 ? 4 : 6, s);
+    } else if constexpr (e == 50) {
+      QZ_G16_STAMP_AT(7, s);
+      // vmcnt(13): the 13 DMAs this step has issued may stay in flight
+      __builtin_amdgcn_s_waitcnt((SK & 1) ? 0xC07F : 0x0F7D);
+      __builtin_amdgcn_s_barrier();
+      QZ_G16_STAMP_AT(8, s);
+    }
+  };
+  if constexpr ((S & 8) != 0) {
+    // Rotated loop: an iteration runs MFMAs [kRot, 128) of step s and [0, kRot) of step s + 1, so
+    // the loop header sits right after a lgkmcnt(0) + barrier -- the compiler's conservative wait at
+    // a loop header then finds no LDS read outstanding (at the step boundary it waited for every
+    // read of step s + 1's k-half 0, ~100 cycles of the MFMA pipe per step).  Step 0's head and the
+    // last step's tail are peeled.
+    constexpr int kRot = 51;
+    static_assert(kGemm4Split.ev[kRot] == 49, "rotate at a lgkmcnt(0) + barrier");
+    auto steps = [&](auto tb) {
+      static_for<kRot>([&](auto nc) { split_mfma(nc, 0, tb); });
+      for (int s = 0; s + 1 < nsteps; ++s) {
+        static_for<128 - kRot>([&](auto nc) {
+          split_mfma(std::integral_constant<int, kRot + decltype(nc)::value>{}, s, tb);
+        });
+        static_for<kRot>([&](auto nc) { split_mfma(nc, s + 1, tb); });
+      }
+      static_for<128 - kRot>([&](auto nc) {
+        split_mfma(std::integral_constant<int, kRot + decltype(nc)::value>{}, nsteps - 1, tb);
+      });
+    };
+    if constexpr ((S & 16) != 0) {
+      // HW_ID bit 4: the low bit of this wave's SIMD
+      if (__builtin_amdgcn_s_getreg((0 << 11) | (4 << 6) | 4) & 1) steps(std::true_type{});
+      else steps(std::false_type{});
+    } else {
+      steps(std::false_type{});
+    }
+  } else
   for (int s = 0; s < nsteps; ++s) {
     const int b = s & 1;
     const int s2 = min(s + 2, nsteps - 1);
     static_for<kNM>([&](auto nc) {
       constexpr int n = decltype(nc)::value;
-      mfma(n / (kNM / 2), n % (kNM / 2));
       if constexpr ((S & 1) != 0) {
-        constexpr int e = kGemm4Split.ev[n + 1];
-        if constexpr (e >= 1 && e <= 8) read_x(b, 1, e - 1);
-        else if constexpr (e >= 9 && e <= 16) read_w(b, 1, e - 9);
-        else if constexpr (e >= 17 && e <= 24) read_x(b ^ 1, 0, e - 17);
-        else if constexpr (e >= 25 && e <= 32) read_w(b ^ 1, 0, e - 25);
-        else if constexpr (e >= 33 && e <= 40) {
-          if constexpr ((SK & 1) == 0) {
-            if (!(S & 4) || s + 2 < nsteps) dma_half(s2, b, e - 33, 0);
-          }
-        } else if constexpr (e >= 41 && e <= 48) {
-          if constexpr ((SK & 1) == 0) {
-            if (!(S & 4) || s + 2 < nsteps) dma_half(s2, b, e - 41, 1);
-          }
-        } else if constexpr (e == 49) {
-          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-          __builtin_amdgcn_s_barrier();
-        } else if constexpr (e == 50) {
-          // vmcnt(13): the 13 DMAs this step has issued may stay in flight.  S & 4 (the last
-          // two steps stage nothing): vmcnt(0) there
-          if ((SK & 1) || ((S & 4) && s + 2 >= nsteps)) __builtin_amdgcn_s_waitcnt(0xC07F);
-          else __builtin_amdgcn_s_waitcnt(0x0F7D);
-          __builtin_amdgcn_s_barrier();
-        }
-        if constexpr (e != 0) __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (n < P1) {
+        split_mfma(nc, s, std::false_type{});
+        return;
+      }
+      if constexpr (n == 0) QZ_G16_STAMP_AT(2, s);
+      if constexpr (n == 0) QZ_G16_STAMP_AT(9, s - 1);
+      mfma(n / (kNM / 2), n % (kNM / 2));
+      if constexpr (n < P1) {
         if constexpr ((n + 1) % kR1 == 0) {
           if constexpr ((SK & 2) == 0) frag_read(b, 1, (n + 1) / kR1 - 1);
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (n == P1 - 1) {
+          QZ_G16_STAMP_AT(3, s);
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
           __builtin_amdgcn_s_barrier();
+          QZ_G16_STAMP_AT(4, s);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else if constexpr (n < P2) {
@@ -1508,8 +1598,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (n == P2 - 1) {
+          QZ_G16_STAMP_AT(7, s);
           __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
           __builtin_amdgcn_s_barrier();
+          QZ_G16_STAMP_AT(8, s);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else if constexpr ((n + 1 - P2) % kR0 == 0) {
@@ -1519,7 +1611,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     });
   }
   if constexpr ((SK & 16) != 0) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  QZ_G16_STAMP(10);
   __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+  QZ_G16_STAMP(11);
 
   if constexpr (kPerm) {
     // ---- epilogue straight from the accumulators: fragments 2J, 2J + 1 of token tile i give a
@@ -1543,6 +1637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = o;
       }
     }
+    QZ_G16_STAMP(12);
     return;
   }
 
@@ -1594,6 +1689,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
   }
+  QZ_G16_STAMP(12);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1991,7 +2087,8 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 
 // QZ_GEMM16_SCHED (read once at load, reported and set through qz_gemv_knobs / qz_gemv_set_knob):
 // the k_gemm16_4d schedule qz_gemm_16bit launches -- 0: P1/P2 segments; S bits: 1 split-release
-// schedule, 2 permuted W rows + 16-B register epilogue, 4 no staging in the last two steps
+// schedule, 2 permuted W rows + 16-B register epilogue, 8 the split schedule's loop rotated, 16 (with 8)
+// the waves on odd SIMDs run the schedule one MFMA later
 namespace qz {
 int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
 }
@@ -2026,7 +2123,10 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
     case 1: QZ_G16(DT_, 1); break;     \
     case 2: QZ_G16(DT_, 2); break;     \
     case 3: QZ_G16(DT_, 3); break;     \
-    case 7: QZ_G16(DT_, 7); break;     \
+    case 9: QZ_G16(DT_, 9); break;     \
+    case 11: QZ_G16(DT_, 11); break;   \
+    case 25: QZ_G16(DT_, 25); break;   \
+    case 27: QZ_G16(DT_, 27); break;   \
     default: QZ_G16(DT_, 0); break;    \
   }
   if (dtype == QZ_DT_F16) {

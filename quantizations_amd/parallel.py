@@ -113,6 +113,18 @@ class RowShardedLinear4bit(nn.Module):
         self.register_buffer("bias", bias, persistent=False)
         self._local_matmul = local_matmul  # test hook; None = the fused HIP kernels
         self.exact_codes = exact_codes_for(getattr(full, "compute_dtype", None))
+        # True (shard_attention_heads, on o_proj): the input is this rank's slice of the features
+        # (its attention heads' output), gathered to the full width before the local rows
+        self.gather_input = False
+
+    def gathered_input(self, x: torch.Tensor) -> torch.Tensor:
+        """x itself, or (gather_input) every rank's slice of it gathered to the full in_features."""
+        if not self.gather_input or self.world_size == 1:
+            return x
+        if x.shape[-1] * self.world_size != self.in_features:
+            raise ValueError(f"head-gathered input: expected {self.in_features // self.world_size} features, "
+                             f"got {x.shape[-1]}")
+        return gather_rows(x, self.world_size, self.group, self.gatherer)
 
     def local_forward(self, x: torch.Tensor) -> torch.Tensor:
         if self._local_matmul is not None:
@@ -138,13 +150,14 @@ class RowShardedLinear4bit(nn.Module):
             return group.take(self, x)
         if group is not None and group.prenorm is not None:
             x = group.prenorm[2](x)      # prefill through a group that absorbed its RMSNorm
-        return self.gather_rows(self.local_forward(x))   # [..., M/P] -> [..., M]
+        return self.gather_rows(self.local_forward(self.gathered_input(x)))   # [..., M/P] -> [..., M]
 
     def forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
         """residual + self(x), for LlamaDecoderLayer's residual adds (integration._project):
         a single token's add rides in the local GEMV's epilogue on this rank's rows
         (qz_gemv_4bit_residual: the same bits as the unsharded layer's fused epilogue), and the
         rows are gathered afterwards.  Anything else: the two-op form."""
+        x_in, x = x, self.gathered_input(x)
         if (self._local_matmul is None and self.gather and x.is_cuda and x.numel() == x.shape[-1]
                 and residual.dtype == x.dtype and residual.device == x.device and residual.is_contiguous()
                 and residual.numel() == self.out_features and residual.shape[:-1] == x.shape[:-1]
@@ -154,7 +167,7 @@ class RowShardedLinear4bit(nn.Module):
             y = gemv_4bit(x, self.packed, state=self.state, bias=self.bias, block_base=self.block_base,
                           exact_codes=self.exact_codes, residual=rows)
             return self.gather_rows(y).reshape(residual.shape)
-        return residual + self(x)
+        return residual + self(x_in)
 
 
 def _group_input(group, x: torch.Tensor, fused_ok: bool):
@@ -413,6 +426,33 @@ def shard_model_linear4bit(model: nn.Module, rank: Optional[int] = None, world_s
         else:
             shard_model_linear4bit(child, rank, world_size, group, local_matmul, gatherer)
     return model
+
+
+def shard_attention_heads(model: nn.Module) -> int:
+    """Head-sharded attention for the row-split layout (after shard_model_linear4bit): each attention
+    module's q/k/v row shards ARE whole heads (rank p's rows [p*M/P, (p+1)*M/P) of q_proj are query
+    heads [p*Hq/P, (p+1)*Hq/P), likewise for k/v and the kv heads), so they stay local (gather=False,
+    no exchange) and the rank runs the attention of its own heads against a KV cache of only its kv
+    heads (transformers takes the head count from the projection width; the StaticCache sizes its
+    layers at the first update).  o_proj then gathers the heads' outputs (gather_input, rank-major =
+    head order) before its row split and its usual exchange.  Per decoder layer: the q/k/v exchange
+    becomes the attention-output exchange, and the replicated attention and KV cache shrink by P.
+    Modules whose heads do not split evenly are left replicated.  Returns the number converted."""
+    n = 0
+    for mod in model.modules():
+        projs = [mod._modules.get(nm) for nm in ("q_proj", "k_proj", "v_proj", "o_proj")]
+        if any(not isinstance(m, RowShardedLinear4bit) for m in projs) or not hasattr(mod, "head_dim"):
+            continue
+        q, k, v, o = projs
+        P, hd = q.world_size, int(mod.head_dim)
+        if P == 1 or any(m.out_features % (hd * P) != 0 for m in (q, k, v)) or \
+                not (q.gather and k.gather and v.gather) or o.in_features != q.out_features:
+            continue
+        for m in (q, k, v):
+            m.gather = False
+        o.gather_input = True
+        n += 1
+    return n
 
 
 class RowShardedDenseLinear(nn.Module):

@@ -5,6 +5,7 @@
 #define QZ_STAMPS8P
 #endif
 #include "../../quantizations_amd/csrc/gemm.hip"
+namespace qz { int &gemm16_sched() { static int v = 0; return v; } }  // the library keeps it in gemv.hip
 
 #include <cstdio>
 #include <cstdlib>

@@ -3,6 +3,7 @@
 // through a wave-private LDS image (TB = token bucket), NF4 + double quant,
 // 16 rotating weight copies, stream parked behind a spin kernel.
 #include "../../quantizations_amd/csrc/gemm.hip"
+namespace qz { int &gemm16_sched() { static int v = 0; return v; } }  // the library keeps it in gemv.hip
 
 #include <cstdio>
 #include <cstdlib>

@@ -1,8 +1,9 @@
 """Low-T prefill route crossover (GPU): gemm_4bit(route="fused") -- the multi-token kernel
 (T <= 16) and the 128-row tile kernel (17 <= T < 4096) -- against route="blas" (dequantize_4bit
 + the library GEMM, the reference's modules.py:62-64), whole-route times including the
-dequant pass, for the four Llama-3-8B shapes.  Sets PREFILL_FUSED_MAX_TOKENS.
-   python scripts/prefill_lowT_sweep.py"""
+dequant pass, for the four Llama-3-8B shapes (default) or the four Llama-3-70B shapes ("70b").  Sets
+core.fused_max_tokens' table.
+   python scripts/prefill_lowT_sweep.py [8b|70b]"""
 import json
 import os
 import sys
@@ -28,7 +29,9 @@ def timed(fn, iters=20):
 
 dev = torch.device("cuda")
 out = {}
-for (M, K) in [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)]:
+SHAPES = {"8b": [(4096, 4096), (1024, 4096), (14336, 4096), (4096, 14336)],
+          "70b": [(8192, 8192), (1024, 8192), (28672, 8192), (8192, 28672)]}
+for (M, K) in SHAPES[sys.argv[1] if len(sys.argv) > 1 else "8b"]:
     torch.manual_seed(M + K)
     packed, st = quantize_4bit((torch.randn(M, K, device=dev) * 0.02).half(), quant_type="nf4")
     for T in (2, 8, 16, 17, 32, 64, 128, 192, 256, 384, 512):

@@ -350,10 +350,16 @@ def _bench_layout_worker(rank, world, port, q, tp_mode, batch, layer_ops="none")
             assert (calls["pair"] > 0) == (batch == 1), calls
         _, ref_hist = bench.decode_bench_graph(ref, cfg, steps=5, warmup=2, prompt_len=6, world=1, batch=batch,
                                                graph=False, device="cpu")
-        q_proj = model.model.layers[0].self_attn.q_proj
+        attn = model.model.layers[0].self_attn
+        up = model.model.layers[0].mlp.up_proj
         from quantizations_amd.parallel import RowShardedDenseLinear
+        # the row split: up_proj gathers its rows; head-sharded attention: q/k/v stay local, o_proj
+        # gathers the heads' outputs first
+        heads = all(isinstance(m, RowShardedLinear4bit) and not m.gather for m in (attn.q_proj, attn.k_proj,
+                                                                                    attn.v_proj)) \
+            and isinstance(attn.o_proj, RowShardedLinear4bit) and attn.o_proj.gather_input and attn.o_proj.gather
         q.put((rank, n_groups, bool(torch.equal(hist, ref_hist)), int((hist[:, 6:13] != 0).sum()),
-               isinstance(q_proj, RowShardedLinear4bit) and q_proj.gather,
+               isinstance(up, RowShardedLinear4bit) and up.gather and heads,
                isinstance(model.get_output_embeddings(), RowShardedDenseLinear)))
     finally:
         dist.destroy_process_group()
@@ -367,7 +373,9 @@ def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops, world):
     """bench.py --gpus N exactly as the driver runs it, on gloo world N (2, 4, 8) with the
     oracle as each shard's local product: the default strong-scaling layout
     (one bs=1 stream, every Linear4bit row-split + all-gather) and the
-    weak-scaling extra (two streams, Megatron pairing).  The greedy tokens of 7
+    weak-scaling extra (two streams, Megatron pairing).  The row split runs the attention
+    head-sharded (each rank's q/k/v rows are whole heads, attended locally; o_proj gathers the
+    heads' outputs).  The greedy tokens of 7
     decode steps equal the unsharded model's on every rank (the row split includes the
     fp16 lm_head: RowShardedDenseLinear).  layer_ops "all": the
     fused decoder layer on the shards (absorbed norms, the sharded SiLU pair, the
@@ -389,7 +397,7 @@ def test_bench_multi_gpu_layout_end_to_end(tp_mode, batch, layer_ops, world):
         assert n_groups == 4, (rank, n_groups)
         assert same, f"rank {rank}: sharded greedy tokens differ from the unsharded model"
         assert n_tok > 0
-        assert gathers == (tp_mode == "gather")
+        assert gathers == (tp_mode == "gather")     # row split + head-sharded attention
         assert head_rows == (tp_mode == "gather")   # the fp16 lm_head row-split too
 
 

@@ -10,7 +10,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda")
-SCHEDS = [1, 2, 3, 7]
+SCHEDS = [1, 2, 3, 9, 11, 25, 27]
 
 
 @pytest.fixture

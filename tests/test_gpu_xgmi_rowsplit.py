@@ -61,8 +61,10 @@ def _work(rank, world, port, q, layout):
         ag = OneShotAllGather(slot_bytes=1 << 18, device=dev)
         if layout.startswith("gather"):
             shard_model_linear4bit(model, rank, world, gatherer=ag)
-            from quantizations_amd.parallel import shard_lm_head
+            from quantizations_amd.parallel import shard_attention_heads, shard_lm_head
             assert shard_lm_head(model, rank, world, gatherer=ag)   # the fp16 lm_head's rows too, as bench.py
+            if "heads" in layout:   # bench.py's default N > 1 layout: every rank attends over its own heads
+                assert shard_attention_heads(model) == cfg.num_hidden_layers
         else:   # Megatron pairing: column q/k/v/gate/up, row o/down with the one-shot all-reduce
             apply_tensor_parallel(model, rank, world, gatherer=ag)
         n_groups = fuse_projection_groups(model)
@@ -108,11 +110,15 @@ def _work(rank, world, port, q, layout):
 
 @pytest.mark.timeout(420)
 @pytest.mark.parametrize("layout,world", [("gather", 2), ("pair", 2), ("gather-fused", 2), ("pair-fused", 2),
-                                          ("gather-fused", 4), ("gather-fused", 8), ("pair-fused", 8)])
+                                          ("gather-fused", 4), ("gather-fused", 8), ("pair-fused", 8),
+                                          ("gather-heads", 2), ("gather-heads-fused", 2), ("gather-heads-fused", 4),
+                                          ("gather-heads-fused", 8)])
 def test_rowsplit_oneshot_on_gpu(layout, world):
     """world 8: config #5's layout with 8 processes on the one MI355X (each mapping the 7 others'
     exchange buffers); gather layouts decode exactly the unsharded model's greedy tokens (a shard's
-    rows are summed in the same order as the unsharded launch's)."""
+    rows are summed in the same order as the unsharded launch's).  gather-heads: bench.py's default
+    N > 1 layout, the attention head-sharded (parallel.shard_attention_heads: local q/k/v heads, a
+    KV cache of the rank's kv heads, the heads' outputs gathered before o_proj)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -639,12 +639,16 @@ def fused_max_tokens(M: int, K: int = 4096) -> int:
     """Largest token count the auto route sends to the fused kernels for an M x K
     weight.  An explicit QZ_PREFILL_FUSED_MAX_T (PREFILL_FUSED_MAX_TOKENS) replaces the
     table.  The table is the measured crossover against dequantize_4bit + hipBLASLt,
-    whole routes (scripts/prefill_lowT_sweep.py, profiles/r2_prefill_lowT_sweep.txt),
-    measured on the Llama-3-8B shapes only (K = 4096 / 14336): 256 tokens for
-    2048..8192 rows, 128 otherwise.  Other K (the 70B shapes, K = 8192 / 28672) take
-    the same rows rule, unmeasured."""
+    whole routes (scripts/prefill_lowT_sweep.py [8b|70b]): the Llama-3-8B shapes
+    (profiles/r2_prefill_lowT_sweep.txt) give 256 tokens for 2048..8192 rows, 128
+    otherwise; the Llama-3-70B shapes (profiles/r6_prefill_lowT_sweep_70b.txt) keep that
+    rule (8192 x 8192 and 8192 x 28672: fused ahead through 256, behind at 384; 28672 x 8192:
+    through 128, behind at 192) except the narrow k/v projections at K = 8192, where the
+    fused kernel stays ahead at every measured T up to 512 (1024 x 8192: 33.7 vs 35.9 us)."""
     if PREFILL_FUSED_MAX_TOKENS is not None:
         return PREFILL_FUSED_MAX_TOKENS
+    if M <= 1024 and K >= 8192:
+        return 512
     return 256 if 2048 <= M <= 8192 else 128
 
 

@@ -252,6 +252,11 @@ def test_fused_route_threshold_follows_measured_crossover():
     assert core.fused_max_tokens(4096) == 256        # 4096x4096, 4096x14336: fused wins to T = 256
     assert core.fused_max_tokens(1024) == 128        # k/v projections: to T = 128
     assert core.fused_max_tokens(14336) == 128       # gate/up: a tie at T = 128, dequant route above
+    # Llama-3-70B (profiles/r6_prefill_lowT_sweep_70b.txt): q/o and down to T = 256, gate/up to 128, and
+    # the k/v projections (1024 x 8192) fused at every measured T up to 512
+    assert core.fused_max_tokens(8192, 8192) == 256 and core.fused_max_tokens(8192, 28672) == 256
+    assert core.fused_max_tokens(28672, 8192) == 128
+    assert core.fused_max_tokens(1024, 8192) == 512 and core.fused_max_tokens(1024, 4096) == 128
     assert core.PREFILL_FUSED_MAX_TOKENS is None     # no QZ_PREFILL_FUSED_MAX_T in the test env
 
 

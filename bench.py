@@ -202,7 +202,7 @@ def decode_bench_graph(model, cfg, steps: int, warmup: int, prompt_len: int, wor
 def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: str = "gather",
                          fuse: bool = True, layer_ops: str = "all", local_matmul=None, gatherer=None,
                          prenorm: bool = True, attention: bool = True, residual: bool = True,
-                         mlp_pair: bool = True, mlp_chain: bool = False,
+                         mlp_pair: bool = True,
                          glue: bool = True, lm_head: bool = True, shard_head: bool = True,
                          head_sharded_attention: bool = True):
     """The bench's model layout after replace_with_bnb_linear: shard every
@@ -241,8 +241,7 @@ def prepare_decode_model(model, rank: int, world: int, sharded: bool, tp_mode: s
                                      mlp=layer_ops in ("all", "all+decoder", "mlp"),
                                      decoder=layer_ops == "all+decoder",
                                      attention=attention and layer_ops in ("all", "all+decoder"),
-                                     residual=residual, mlp_pair=mlp_pair,
-                                     mlp_chain=mlp_chain)  # one launch each
+                                     residual=residual, mlp_pair=mlp_pair)  # one launch each
     if prenorm and fuse and layer_ops in ("all", "norm"):
         from quantizations_amd.integration import fuse_prenorm
         n_layer_ops += fuse_prenorm(model)   # RMSNorm inside the q/k/v and gate/up launches
@@ -561,8 +560,7 @@ def dominant_roofline(copies: int = 8, iters: int = 100, prenorm: bool = True, p
 
 
 @torch.inference_mode()
-def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b",
-                   mlp_chain: bool = False):
+def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: int = 1, model_name: str = "llama3-8b"):
     """The Linear4bit chain of a Llama-3 decoder layer as the bench decode runs it -- q/k/v
     (+ input RMSNorm) grouped, o_proj (+ residual), gate/up + SiLU (+ post-attention RMSNorm)
     paired, down_proj (+ residual) -- four dependent launches per layer, `layers` layers on
@@ -573,13 +571,10 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     q output in its place, so every launch still depends on the previous one).  Where the product
     takes another form (Llama-3-70B: gate/up at K = 8192 splits rows over two waves, so the split
     pair runs after a separate norm launch), the chain runs what the product runs; `gate_up_form` and
-    `launches_per_layer` say which.  mlp_chain (one GPU): o_proj + residual, the
-    norm, gate/up + SiLU and down_proj + residual as the ONE persistent launch the product runs
-    (core.gemv_4bit_mlp_chain), so a layer is two launches.  shards = P > 1: the same chain on ONE rank's
+    `launches_per_layer` say which.  shards = P > 1: the same chain on ONE rank's
     rows of the row-split layout (every projection M / P rows, the launches a rank runs per layer
     at N = P; the exchanges are timed separately), for the N-GPU budget in DESIGN.md section 6."""
-    from quantizations_amd.core import (LAST_FORM, gemv_4bit, gemv_4bit_grouped, gemv_4bit_mlp_chain,
-                                        gemv_4bit_pair_silu, mlp_chain_state, quantize_4bit)
+    from quantizations_amd.core import LAST_FORM, gemv_4bit, gemv_4bit_grouped, gemv_4bit_pair_silu, quantize_4bit
     from quantizations_amd.layer_ops import silu_mul
 
     base_cfg = MODELS[model_name]
@@ -615,21 +610,12 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
     full_h = torch.randn(1, 1, I, device=dev).half()
     forms = set()
     launches = []   # per layer, as the forms ran (a norm launch counts)
-    use_chain = mlp_chain and shards == 1
-    cstate = mlp_chain_state(dev) if use_chain else None
 
     def layer(x, w):
         q, _, _ = gemv_4bit_grouped(x, [(*w["q"], None, 0, qkv_out[0]), (*w["k"], None, 0, qkv_out[1]),
                                         (*w["v"], None, 0, qkv_out[2])], exact_codes=True, norm=(nw1, 1e-5))
         n = 2 if LAST_FORM.get("grouped", "").startswith("norm launch") else 1
         forms.add("q/k/v " + LAST_FORM.get("grouped", "?"))
-        if use_chain:
-            y = gemv_4bit_mlp_chain(q.view(1, 1, H), x.view(1, 1, H), (*w["o"], None), (*w["gate"], None),
-                                    (*w["up"], None), (*w["down"], None), (nw2, 1e-5), cstate, exact_codes=True)
-            if y is not None:
-                forms.add("o/norm/gate/up/down as ONE persistent launch (qz_mlp_chain)")
-                launches.append(n + 1)
-                return y
         xo = q.view(1, 1, H) if shards == 1 else x          # o_proj reads the (gathered) attention output
         a = gemv_4bit(xo, w["o"][0], state=w["o"][1], exact_codes=True, residual=x.view(-1)[:Hs])
         xa = a if shards == 1 else x                        # ... the gathered residual stream
@@ -680,7 +666,6 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
               + gemv_alg_bytes([(Is, H)] * 2) - 2 * H - 2 * Is                  # pair: x once, one output
               + gemv_alg_bytes([(Hs, I)]) + 2 * Hs                              # down_proj + its residual read
               + 2 * (2 * H))                                                    # the two RMSNorm weights
-    failed = bool(cstate[-32].item()) if cstate is not None else False
     del sets, g
     torch.cuda.empty_cache()
     ach = nbytes / (us * 1e-6) / 1e9
@@ -691,7 +676,6 @@ def chain_roofline(copies: int = 8, layers: int = 32, reps: int = 10, shards: in
                     + (f"; ONE rank's rows of the {shards}-way row split (exchanges not included)" if shards > 1 else ""),
             "model": model_name, "shards": shards, "gate_up_form": sorted(forms),
             "launches_per_layer": max(launches) if launches else None,
-            "chain_barrier_gave_up": failed,
             "us_per_layer": round(us, 3), "algorithmic_bytes_per_layer": nbytes,
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_layer_min": round(min(times), 3), "us_per_layer_max": round(max(times), 3)}
@@ -1131,9 +1115,6 @@ def main():
     ap.add_argument("--prefill-only", action="store_true", help="only the config #4 prefill GEMM measurement")
     ap.add_argument("--chain-only", action="store_true",
                     help="only the Linear4bit chain of one decoder layer (chain_roofline; profiling)")
-    ap.add_argument("--chain-persistent", action="store_true",
-                    help="--chain-only: o_proj .. down_proj as the ONE persistent launch (csrc/chain.hip) instead of the "
-                         "product's three launches")
     ap.add_argument("--chain-shards", type=int, default=1,
                     help="--chain-only: the chain on one rank's rows of a P-way row split")
     ap.add_argument("--dominant-only", action="store_true",
@@ -1156,10 +1137,6 @@ def main():
                          "stages, the same index)")
     ap.add_argument("--no-mlp-pair", action="store_true",
                     help="gate/up as the grouped launch + a separate SiLU-product launch (default: one launch)")
-    ap.add_argument("--mlp-chain", action="store_true",
-                    help="run o_proj + residual, gate/up + SiLU (+ norm) and down_proj + residual as ONE persistent "
-                         "launch per layer (csrc/chain.hip; measured slower than the default three launches: its grid "
-                         "barriers cost more than launch boundaries, DESIGN.md section 12)")
     ap.add_argument("--lm-head-library", action="store_true",
                     help="keep the fp16 lm_head on F.linear (hipBLASLt) instead of layer_ops.gemv_dense (its "
                          "rows stay split over the ranks; --no-shard-lm-head replicates it)")
@@ -1251,8 +1228,7 @@ def main():
         print(json.dumps(dominant_roofline()), flush=True)
         return
     if args.chain_only:
-        print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model,
-                                        mlp_chain=args.chain_persistent)), flush=True)
+        print(json.dumps(chain_roofline(shards=args.chain_shards, model_name=args.model)), flush=True)
         return
     if args.prefill_only:
         print(json.dumps(prefill_bench()), flush=True)
@@ -1267,8 +1243,6 @@ def main():
     global GREEDY
     GREEDY = "torch" if args.torch_argmax else args.greedy
 
-    chain_faults = {}
-
     def run_decode(tp_mode: str, gbatch: int, steps: int, warmup: int, cdt: torch.dtype = compute_dtype):
         t_build = time.perf_counter()
         model, cfg = build_model(args.layers, seed=0, model_name=args.model, quant_type=args.quant,
@@ -1281,7 +1255,6 @@ def main():
                                                      attention=not args.no_attention,
                                                      residual=not args.no_residual,
                                                      mlp_pair=not args.no_mlp_pair,
-                                                     mlp_chain=args.mlp_chain,
                                                      glue=not args.no_glue,
                                                      lm_head=not args.lm_head_library,
                                                      shard_head=not args.no_shard_lm_head,
@@ -1298,9 +1271,6 @@ def main():
                 torch.cuda.synchronize()
         if mode == "eager":
             dt, _ = decode_bench(model, cfg, steps, warmup, args.prompt, world, gbatch)
-        if args.mlp_chain:   # a chain that gave up at a grid barrier left untrustworthy outputs: say so
-            from quantizations_amd.integration import mlp_chain_faults
-            chain_faults[tp_mode] = mlp_chain_faults(model, disable=True)
         t = torch.tensor([dt], device="cuda")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)   # the slowest rank's time
@@ -1344,7 +1314,7 @@ def main():
     if rank == 0 and not args.no_roofline:
         roof = _safe(roofline_object, args, layer_ops)
         parity = _safe(gemv_parity)
-        chain = _safe(chain_roofline, mlp_chain=args.mlp_chain)
+        chain = _safe(chain_roofline)
 
     layer = None
     if not args.no_roofline:
@@ -1397,11 +1367,6 @@ def main():
                                                         and layer_ops in ("all", "all+decoder", "mlp"))
         line["config"]["residual_in_gemv_epilogue"] = bool(not args.no_residual and not args.no_attention
                                                            and layer_ops == "all")
-        line["config"]["mlp_chain_launch"] = bool(args.mlp_chain and not args.no_residual and not args.no_attention
-                                                  and not args.no_prenorm and not args.no_fuse and layer_ops == "all"
-                                                  and not sharded)
-        if args.mlp_chain:
-            line["config"]["mlp_chain_faults"] = chain_faults   # layers whose chain gave up (0 = valid run)
         line["config"]["lm_head"] = "F.linear (hipBLASLt)" if (args.lm_head_library or layer_ops == "none") \
             else "layer_ops.gemv_dense"
         line["config"]["lm_head_rows_split"] = bool(sharded and tp_mode == "gather" and not args.no_shard_lm_head)

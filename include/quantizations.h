@@ -366,26 +366,6 @@ int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, in
                            int blocksize, int blocksize2, const float *lut, const void *norm_weight, float eps,
                            void *h, void *stream);
 
-/* LlamaDecoderLayer's MLP half (modeling_llama.py:316-322 on the fused modules) as ONE persistent
- * launch (round 5, not in the reference; csrc/chain.hip):
- *   h1  = residual + o_proj(x)                                  -> h1  [H] (scratch)
- *   act = silu(gate_proj(rmsnorm(h1))) * up_proj(rmsnorm(h1))   -> act [I] (scratch)
- *   out = h1 + down_proj(act)                                   -> out [H]
- * o / down: M = H / H rows, gate / up: M = I rows (their y fields are ignored).  x, residual, out,
- * h1, act and norm_weight are F16 or BF16 `dtype` vectors (16-B aligned; h1 and act distinct from
- * every other buffer).  Bit-identical to qz_gemv_4bit_residual(o) -> qz_gemv_4bit_pair_silu(gate,
- * up, norm) -> qz_gemv_4bit_residual(down).  One workgroup per CU, grid barriers between the
- * stages; `state` = qz_mlp_chain_state_words() int32 words, zeroed ONCE before the first call and
- * then owned by the calls (one state per stream that runs chains concurrently).  Shapes it does not
- * take (K not a multiple of 2048, H > 8192, rows not multiples of 8, a runtime codebook): QZ_ERR_SHAPE,
- * nothing launched.  If a grid barrier ever gives up (a workgroup not resident), the call still ends
- * and the word qz_mlp_chain_state_words() - 32 of `state` becomes nonzero. */
-int qz_mlp_chain(const qz_gemv_segment *o, const qz_gemv_segment *gate, const qz_gemv_segment *up,
-                 const qz_gemv_segment *down, const void *x, const void *residual, int dtype, int quant_type,
-                 int blocksize, int blocksize2, const void *norm_weight, float eps, void *h1, void *act, void *out,
-                 unsigned *state, void *stream);
-int qz_mlp_chain_state_words(void);
-
 /* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
  * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1, and QZ_GEMM16_SCHED -- the k_gemm16_4d schedule qz_gemm_16bit
  * launches: environment variables read ONCE when the library is loaded) and the

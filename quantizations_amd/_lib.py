@@ -96,8 +96,6 @@ SIGNATURES = {
     "qz_allgather_oneshot_mode": [_p, _i, _p, _i, _i, _p, _p, _ll, _p, _p, _i, _p],
     "qz_gemv_knobs": [_p, _i],
     "qz_gemv_set_knob": [ctypes.c_char_p, _i],
-    "qz_mlp_chain": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _f, _p, _p, _p, _p, _p],
-    "qz_mlp_chain_state_words": [],
     "qz_version": [],
 }
 RESTYPES = {"qz_absmax_mean_workspace": _ll, "qz_gemm_4bit_workspace_size": _ll, "qz_exchange_bytes": _ll,

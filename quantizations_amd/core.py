@@ -501,61 +501,6 @@ def gemv_4bit_pair_silu(A: Tensor, items, exact_codes: Optional[bool] = None, no
     return h
 
 
-def mlp_chain_state(device) -> Tensor:
-    """Sync state of qz_mlp_chain (int32 words, zeroed once; one per stream running chains)."""
-    return torch.zeros(int(lib.qz_mlp_chain_state_words()), dtype=torch.int32, device=device)
-
-
-def mlp_chain_failed(state: Tensor) -> bool:
-    """True once a qz_mlp_chain call on `state` gave up waiting at a grid barrier (synchronises)."""
-    return bool(state[-32].item())
-
-
-def gemv_4bit_mlp_chain(x: Tensor, residual: Tensor, o, gate, up, down, norm, state: Tensor,
-                        exact_codes: Optional[bool] = None) -> Optional[Tensor]:
-    """LlamaDecoderLayer's MLP half for one token in ONE persistent launch (qz_mlp_chain):
-    out = h1 + down(silu(gate(rms(h1))) * up(rms(h1))) with h1 = residual + o(x), where o, gate, up
-    and down are (B, state, bias[, block_base]) items and norm = (weight, eps) the post-attention
-    RMSNorm.  Bit-identical to gemv_4bit(o, residual=...) -> gemv_4bit_pair_silu(norm=...) ->
-    gemv_4bit(down, residual=h1).  `state`: mlp_chain_state(device).  Returns None for what the
-    kernel does not take (the caller runs the three launches)."""
-    items = [tuple(it) + (0,) * (4 - len(it)) for it in (o, gate, up, down)]
-    if x.numel() != x.shape[-1] or x.dtype not in (torch.float16, torch.bfloat16) or not x.is_cuda:
-        return None
-    so, sg, su, sd = (it[1] for it in items)
-    H, I = so.shape[0], sg.shape[0]
-    if (so.shape[1] != H or sg.shape != su.shape or sg.shape[1] != H or tuple(sd.shape) != (H, I)
-            or residual.numel() != H or residual.dtype != x.dtype or not residual.is_contiguous()
-            or residual.device != x.device):
-        return None
-    if any(s.quant_type != so.quant_type or s.blocksize != so.blocksize or s.nested != so.nested
-           or (s.nested and s.state2.blocksize != so.state2.blocksize) for s in (sg, su, sd)):
-        return None
-    nw, eps = norm
-    if not (nw.dtype == x.dtype and nw.is_cuda and nw.is_contiguous() and nw.numel() == H):
-        return None
-    x = x.contiguous()
-    segs = (_lib.GemvSegment * 4)()
-    for i, (B, st, bias, block_base) in enumerate(items):
-        if bias is not None and bias.dtype != x.dtype:
-            bias = bias.to(x.dtype)
-        am, qam, am2, code2, off, _ = st.scale_args()
-        segs[i] = _lib.GemvSegment(st.shape[0], ptr(B), am, qam, am2, code2, off, int(block_base), ptr(bias), None)
-    h1 = torch.empty(H, dtype=x.dtype, device=x.device)
-    act = torch.empty(I, dtype=x.dtype, device=x.device)
-    out = torch.empty(residual.shape, dtype=x.dtype, device=x.device)
-    bs2 = int(so.state2.blocksize) if so.nested else 0
-    base = ctypes.cast(segs, ctypes.c_void_p).value
-    sz = ctypes.sizeof(_lib.GemvSegment)
-    rc = lib.qz_mlp_chain(base, base + sz, base + 2 * sz, base + 3 * sz, ptr(x), ptr(residual), dtype_code(x.dtype),
-                          _gemv_quant_type(so.quant_type, exact_codes, x.dtype), so.blocksize, bs2, ptr(nw), float(eps),
-                          ptr(h1), ptr(act), ptr(out), ptr(state), _lib.stream_of(x))
-    if rc == _lib.QZ_ERR_SHAPE:
-        return None
-    check(rc, "gemv_4bit_mlp_chain")
-    return out
-
-
 def gemv_4bit_grouped(A: Tensor, items, exact_codes: Optional[bool] = None, norm=None) -> list:
     """Several batch-1 4-bit GEMVs that share the input vector A, in ONE launch
     (qz_gemv_4bit_grouped).  items: sequence of

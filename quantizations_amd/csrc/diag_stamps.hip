@@ -7,7 +7,6 @@
 // included product entry points of gemv.hip never clash with libquantizations.so.
 #define QZ_STAMPS 1
 #include "gemv.hip"
-#include "chain.hip"
 
 #define QZ_DIAG_API extern "C" __attribute__((visibility("default")))
 
@@ -51,21 +50,3 @@ QZ_DIAG_API int qz_diag_gemv_stamped(int M, int K, const void *x, const unsigned
   return QZ_OK;
 }
 
-// The product qz_mlp_chain with stage stamps (12 u64 per workgroup: chain.hip CH_STAMP points) into
-// `buf`; *grid = the workgroups launched.
-QZ_DIAG_API int qz_diag_mlp_chain_stamped(const qz_gemv_segment *o, const qz_gemv_segment *gate,
-                                          const qz_gemv_segment *up, const qz_gemv_segment *down, const void *x,
-                                          const void *residual, int dtype, int quant_type, int blocksize,
-                                          int blocksize2, const void *norm_weight, float eps, void *h1, void *act,
-                                          void *out, unsigned *state, unsigned long long *buf, int *grid,
-                                          void *stream) {
-  ChainArgs c;
-  bool cl, dq;
-  size_t lds;
-  const int rc = chain_args(o, gate, up, down, x, residual, dtype, quant_type, blocksize, blocksize2, norm_weight, eps,
-                            h1, act, out, state, &c, &cl, &dq, &lds);
-  if (rc != QZ_OK) return rc;
-  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_qz_chain_stamp), &buf, sizeof(buf));
-  if (e != hipSuccess) return (int)e;
-  return chain_launch<1>(c, dtype, cl, dq, lds, (hipStream_t)stream, grid);
-}

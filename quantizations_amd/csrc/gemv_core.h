@@ -1,6 +1,6 @@
 // gemv_core.h -- the decode GEMV's device core (byte tables, step loads, the GEMV body) and the
-// host-side geometry / argument helpers, shared by gemv.hip (the per-layer launches) and chain.hip
-// (the persistent MLP half-layer).  See gemv.hip's header for the design.
+// host-side geometry / argument helpers of gemv.hip (the per-layer launches), also built into the
+// measurement-only diag library and the microbenchmarks.  See gemv.hip's header for the design.
 #pragma once
 #include "common.h"
 

@@ -259,88 +259,17 @@ def _fused_mlp_forward(mod: nn.Module, pair: bool = True):
     return forward
 
 
-def _mlp_chain(layer: nn.Module, x: torch.Tensor, residual: torch.Tensor):
-    """The layer's o_proj + residual, post-attention RMSNorm, gate/up + SiLU and down_proj + residual
-    for one token as ONE persistent launch (core.gemv_4bit_mlp_chain, bit-identical to the three
-    launches it replaces), or None where it does not apply: the four projections must be plain
-    Linear4bit layers of one format, gate/up a decode group that absorbed the post-attention norm
-    (fuse_prenorm), o_proj and down_proj ungrouped, x a single token the layers decode on their own."""
-    from .core import exact_codes_for, gemv_4bit_mlp_chain, mlp_chain_state
-
-    attn, mlp = layer.self_attn, layer.mlp
-    o, g, u, d = attn.o_proj, mlp.gate_proj, mlp.up_proj, mlp.down_proj
-    if any(type(m) is not Linear4bit or m.weight.quant_state is None for m in (o, g, u, d)):
-        return None
-    grp = g.__dict__.get("_qz_group")
-    if grp is None or grp._compute is not _linear4bit_group_compute or grp.prenorm is None or \
-            [id(m) for m in grp.members] != [id(g), id(u)] or "_qz_group" in o.__dict__ or "_qz_group" in d.__dict__:
-        return None
-    if not (x.is_cuda and x.numel() == x.shape[-1] and x.dtype in (torch.float16, torch.bfloat16)):
-        return None
-    for m in (o, g, u, d):
-        if not m.compute_type_is_set:
-            m.set_compute_type(x)
-            m.compute_type_is_set = True
-        if m._input(x) is not x:
-            return None
-    ex = exact_codes_for(o.compute_dtype)
-    if any(exact_codes_for(m.compute_dtype) != ex for m in (g, u, d)):
-        return None
-    st = layer.__dict__.get("_qz_chain_state")
-    if st is None or st.device != x.device:
-        st = mlp_chain_state(x.device)
-        layer.__dict__["_qz_chain_state"] = st
-
-    def item(m):
-        return (m.weight, m.weight.quant_state, None if m.bias is None else m.bias.to(x.dtype))
-    return gemv_4bit_mlp_chain(x, residual, item(o), item(g), item(u), item(d), grp.prenorm[:2], st, exact_codes=ex)
-
-
-def mlp_chain_faults(model: nn.Module, disable: bool = True) -> int:
-    """How many layers' persistent MLP chains (fuse_layer_ops(mlp_chain=True)) ever gave up waiting at a
-    grid barrier (core.mlp_chain_failed: the launch then ends with outputs that cannot be trusted).
-    Synchronises.  With `disable`, a fault turns the chain off in every layer (the three launches run
-    from then on); callers check after a warm-up and again after a timed run."""
-    from .core import mlp_chain_failed
-
-    bad = 0
-    layers = [m for m in model.modules() if "_qz_mlp_chain" in m.__dict__]
-    for m in layers:
-        st = m.__dict__.get("_qz_chain_state")
-        if st is not None and mlp_chain_failed(st):
-            bad += 1
-    if bad and disable:
-        for m in layers:
-            m.__dict__["_qz_mlp_chain"] = False
-    return bad
-
-
 def _residual_decoder_forward(mod: nn.Module):
     """LlamaDecoderLayer.forward (modeling_llama.py:295-324) with both `residual + h` adds
     moved into the epilogues of the o_proj and down_proj GEMVs (their modules were patched by
     fuse_layer_ops and take `_qz_residual`); the norms are called as the model has them (an
-    identity once fuse_prenorm absorbed them).  Bit-identical to the original.  With the MLP
-    chain (fuse_layer_ops(mlp_chain=True)), a decode token's o_proj + residual, post-attention
-    norm, MLP and second residual run as ONE persistent launch (_mlp_chain): the attention module
-    hands its output to `tail` instead of projecting it."""
+    identity once fuse_prenorm absorbed them).  Bit-identical to the original."""
     def forward(hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
                 position_embeddings=None, **kwargs):
         h = mod.input_layernorm(hidden_states)
-        done = []
-        tail = None
-        if mod.__dict__.get("_qz_mlp_chain"):
-            def tail(attn_out, residual):
-                out = _mlp_chain(mod, attn_out, residual)
-                if out is not None:
-                    done.append(out)
-                    return out
-                return _project(mod.self_attn.o_proj, attn_out, residual)
         hidden_states, _ = mod.self_attn(hidden_states=h, attention_mask=attention_mask, position_ids=position_ids,
                                          past_key_values=past_key_values, use_cache=use_cache,
-                                         position_embeddings=position_embeddings, _qz_residual=hidden_states,
-                                         _qz_o_tail=tail, **kwargs)
-        if done:
-            return done[0]
+                                         position_embeddings=position_embeddings, _qz_residual=hidden_states, **kwargs)
         h = mod.post_attention_layernorm(hidden_states)
         return mod.mlp(h, _qz_residual=hidden_states)
     return forward
@@ -365,9 +294,8 @@ def _fused_attention_forward(mod: nn.Module, orig):
     from .layer_ops import decode_attention, decode_attention_supported
 
     def forward(hidden_states, position_embeddings=None, attention_mask=None, past_key_values=None,
-                _qz_residual=None, _qz_o_tail=None, **kwargs):
-        # _qz_residual (the residual-fused decoder layer): return residual + attention output;
-        # _qz_o_tail(attention output, residual): what replaces o_proj + residual on the decode path
+                _qz_residual=None, **kwargs):
+        # _qz_residual (the residual-fused decoder layer): return residual + attention output
         layer = None
         if (hidden_states.dim() == 3 and hidden_states.shape[1] == 1 and position_embeddings is not None
                 and not kwargs.get("output_attentions", False) and not mod.training
@@ -393,8 +321,6 @@ def _fused_attention_forward(mod: nn.Module, orig):
                     return (h if _qz_residual is None else _qz_residual + h), w
                 out = decode_attention(q, k, v, cos, sin, layer.keys, layer.values, attention_mask,
                                        layer.cumulative_length, arrive, nq, mod.scaling)
-                if _qz_o_tail is not None and _qz_residual is not None:
-                    return _qz_o_tail(out, _qz_residual), None
                 return _project(mod.o_proj, out, _qz_residual), None
         h, w = orig(hidden_states, position_embeddings, attention_mask, past_key_values, **kwargs)
         return (h if _qz_residual is None else _qz_residual + h), w
@@ -436,7 +362,7 @@ def _fused_decoder_forward(mod: nn.Module):
 
 def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: bool = True,
                    decoder: bool = False, attention: bool = True, residual: bool = True,
-                   mlp_pair: bool = True, mlp_chain: bool = False) -> int:
+                   mlp_pair: bool = True) -> int:
     """Route every Llama-style RMSNorm of `model`, the rotary embedding of its
     attention modules, the SiLU-gate product of its MLPs and each decoder
     layer's residual add + post-attention norm through one HIP launch each
@@ -451,11 +377,7 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
     once per module).  `residual` (with `attention` and `mlp`) moves each decoder layer's two
     residual adds into the o_proj / down_proj GEMV epilogues (counted once per layer).
     `mlp_pair` lets a fused MLP compute gate/up and act_fn(gate) * up in one launch
-    (modules.linear4bit_silu_pair) where its projections form a decode group.  `mlp_chain` (opt-in,
-    with `residual`) lets a residual-fused decoder layer run a decode token's o_proj + residual,
-    post-attention norm, MLP and second residual as ONE persistent launch (_mlp_chain) where the
-    layer qualifies (after fuse_prenorm): bit-identical, but measured slower than the three launches
-    (each in-kernel grid barrier costs 6-7 us against a ~1.5 us launch boundary)."""
+    (modules.linear4bit_silu_pair) where its projections form a decode group."""
     import sys
 
     n = 0
@@ -499,7 +421,6 @@ def fuse_layer_ops(model: nn.Module, norm: bool = True, rope: bool = True, mlp: 
                     "_qz_fused_mlp" in getattr(m, "mlp", nn.Module()).__dict__:
                 m.__dict__["forward"] = _residual_decoder_forward(m)
                 m.__dict__["_qz_residual_decoder"] = True
-                m.__dict__["_qz_mlp_chain"] = bool(mlp_chain)
                 n += 1
     return n
 
@@ -516,8 +437,6 @@ def unfuse_layer_ops(model: nn.Module) -> None:
                 m.__dict__.pop("_qz_residual_decoder", None):
             m.__dict__.pop("forward", None)
             m.__dict__.pop("_qz_attn_arrive", None)
-            m.__dict__.pop("_qz_mlp_chain", None)
-            m.__dict__.pop("_qz_chain_state", None)
     for modname, fn in list(_ROPE_PATCHED.items()):
         setattr(sys.modules[modname], "apply_rotary_pos_emb", fn)
         del _ROPE_PATCHED[modname]

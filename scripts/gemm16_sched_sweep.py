@@ -14,6 +14,17 @@ from quantizations_amd import _lib  # noqa: E402
 from quantizations_amd.core import gemm_16bit  # noqa: E402
 
 ROUNDS = int(os.environ.get("ROUNDS", "7"))
+# DATA=uniform: gemm16_stamps.hip's operands (fp16 bits (h & 0x83FF) | 0x3800: |v| in [0.5, 1), random sign
+# and mantissa) instead of randn -- the chip's clock under load depends on the operands' bits
+DATA = os.environ.get("DATA", "randn")
+
+
+def operand(rows, cols, scale):
+    if DATA == "uniform":
+        h = torch.randint(0, 1 << 16, (rows, cols), device="cuda", dtype=torch.int32)
+        v = (h & 0x83FF) | 0x3800
+        return torch.where(v >= 32768, v - 65536, v).to(torch.int16).view(torch.float16)
+    return (torch.randn(rows, cols, device="cuda") * scale).half()
 scheds = [int(s) for s in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 3, 9, 11]
 
 
@@ -32,8 +43,8 @@ dev = torch.device("cuda")
 out = {}
 for (M, K, T) in [(4096, 4096, 16384), (14336, 4096, 16384), (4096, 14336, 16384), (4096, 4096, 4096)]:
     torch.manual_seed(M + K + T)
-    W = (torch.randn(M, K, device=dev) * 0.02).half()
-    x = torch.randn(T, K, device=dev, dtype=torch.float16)
+    W = operand(M, K, 0.02)
+    x = operand(T, K, 1.0)
     iters = max(2, int(2e12 / (2.0 * T * M * K) * 3))
     ys = {}
     for s in scheds:

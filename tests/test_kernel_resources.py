@@ -77,16 +77,13 @@ def test_decode_gemv_kernels_fit_without_spills():
         base = name.split("<")[0].replace("void ", "").strip()
         a = _targs(name)
         # every decode kernel's template starts <DQ, DT, R, ...>
-        if base not in ("qz::k_gemv_4bit", "qz::k_gemv_4bit_grouped", "qz::k_gemv_4bit_pair", "qz::k_mlp_chain") \
-                or len(a) < 4:
+        if base not in ("qz::k_gemv_4bit", "qz::k_gemv_4bit_grouped", "qz::k_gemv_4bit_pair") or len(a) < 4:
             continue
-        dt, r = int(a[1]), int(a[3] if base == "qz::k_mlp_chain" else a[2])   # k_mlp_chain<DQ, DT, CL, R>
+        dt, r = int(a[1]), int(a[2])
         if dt not in (0, 1) or r > 4:   # 16-bit activations (F16 = 0, BF16 = 1), up to 4 rows per wave
             continue
         checked += 1
-        # the persistent MLP chain keeps three stages' loop parameters: its few SGPR spills live in
-        # VGPR lanes outside the step loops (checked in its .s); everything else spills nothing
-        if agpr > 0 or priv > 0 or vgpr > 256 or vsp or (ssp and base != "qz::k_mlp_chain"):
+        if agpr > 0 or priv > 0 or vgpr > 256 or vsp or ssp:
             bad.append((vgpr, agpr, priv, ssp, vsp, name))
     assert checked > 50, f"only {checked} decode GEMV kernels found in the code objects"
     assert not bad, "decode GEMV kernels that spill:\n" + "\n".join(map(str, sorted(bad, reverse=True)[:20]))

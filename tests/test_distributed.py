@@ -469,3 +469,29 @@ def test_row_parallel_fp32_allreduce_within_fp16_rounding():
     for rank, is_half, same in res:
         assert is_half
         assert same, f"rank {rank}: row-parallel output is not the fp32 sum of the fp16 partials"
+
+
+def test_shard_attention_heads_and_tied_lm_head_rules():
+    """CPU, no collective: shard_attention_heads keeps q/k/v row shards local and makes o_proj gather its
+    input only where every projection's rows are whole heads on each rank (world 2: 4 q / 2 kv heads split;
+    world 8: 2 kv heads of 32 do not -- left replicated); shard_lm_head refuses a head tied to the input
+    embedding (the embedding stays whole, and tie_weights() would undo the split)."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from quantizations_amd.parallel import (RowShardedDenseLinear, RowShardedLinear4bit, shard_attention_heads,
+                                            shard_lm_head, shard_model_linear4bit)
+
+    for world, expect in ((2, 2), (8, 0)):
+        cfg, model, _ = _tiny_llama_4bit(2)
+        shard_model_linear4bit(model, 0, world)
+        assert shard_attention_heads(model) == expect
+        attn = model.model.layers[0].self_attn
+        assert all(isinstance(m, RowShardedLinear4bit) for m in (attn.q_proj, attn.k_proj, attn.v_proj, attn.o_proj))
+        assert attn.q_proj.gather == (expect == 0) and attn.o_proj.gather_input == (expect > 0)
+        assert model.model.layers[0].mlp.up_proj.gather   # the MLP keeps the plain row split
+    for tied in (False, True):
+        cfg = LlamaConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=1, num_attention_heads=2,
+                          num_key_value_heads=2, vocab_size=96, tie_word_embeddings=tied)
+        model = LlamaForCausalLM(cfg).eval()
+        assert shard_lm_head(model, 0, 2) == (not tied)
+        assert isinstance(model.get_output_embeddings(), RowShardedDenseLinear) == (not tied)

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <hip/hip_fp16.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -137,6 +138,20 @@ __device__ __forceinline__ float dq_scale(const ScaleSrc &s, long long b, float 
 
 inline bool valid_blocksize(int bs) {
   return bs == 64 || bs == 128 || bs == 256 || bs == 512 || bs == 1024 || bs == 2048 || bs == 4096;
+}
+
+// Compute units of the current device (hipDeviceGetAttribute), cached per device: the persistent
+// grids are sized in workgroups per CU.
+static int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v <= 0) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
 }
 
 }  // namespace qz

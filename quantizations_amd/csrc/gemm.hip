@@ -33,6 +33,7 @@
 // return QZ_ERR_SHAPE and the host falls back to dequantize + library GEMM.
 #include "common.h"
 #include "decode.h"
+#include "gemm16_asm_step.h"
 
 namespace qz {
 
@@ -1539,7 +1540,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       QZ_G16_STAMP_AT(8, s);
     }
   };
-  if constexpr ((S & 8) != 0) {
+  if constexpr ((S & 64) != 0) {
+    // Each step ONE hand-ordered instruction stream (gemm16_asm_step.h, generated by
+    // scripts/gen/gemm16_asm_step.py): the same MFMAs on the same accumulators in the same order
+    // (bit-identical), the reads / DMAs / waits / barriers exactly where the schedule puts them, and no
+    // wait the compiler would add.  S & 128: the library's two event orders, by the SIMD's low bit
+    // (else kGemm4Split's); S & 2: the permuted W rows of the register epilogue.  Two buffers
+    // alternate: a step reads its k-half 1 fragments from buffer b, the next step's k-half 0 from
+    // b ^ 1, and refills b by DMA.
+    typedef __attribute__((address_space(3))) unsigned char lds_uc;
+    const uint32_t sb = (uint32_t)(uintptr_t)(lds_uc *)smem;
+    // HW_ID bits 4..5: this wave's SIMD; DUAL runs the library's L1 order on odd SIMDs, L0 on even
+    const uint32_t simd_odd = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg((0 << 11) | (4 << 6) | 4) & 1);
+    uint32_t xb1[2], wb1[2], xb0[2], wb0[2], mb[2];
+#pragma unroll
+    for (int buf = 0; buf < 2; ++buf) {
+      const uint32_t bb = sb + (uint32_t)(buf * k4dBuf);
+      xb1[buf] = bb + fl[1] + (uint32_t)(128 * wt) * 128u;
+      xb0[buf] = bb + fl[0] + (uint32_t)(128 * wt) * 128u;
+      wb1[buf] = bb + (uint32_t)k4wStage + (kPerm ? wl[1] : fl[1]) + (uint32_t)(128 * wm) * 128u;
+      wb0[buf] = bb + (uint32_t)k4wStage + (kPerm ? wl[0] : fl[0]) + (uint32_t)(128 * wm) * 128u;
+      mb[buf] = __builtin_amdgcn_readfirstlane(bb + 1024u * (uint32_t)wave);
+    }
+#define QZ_G16_ASM_OPS(B_)                                                                                        \
+  : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[0][4]), "+a"(acc[0][5]),          \
+    "+a"(acc[0][6]), "+a"(acc[0][7]), "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3]),          \
+    "+a"(acc[1][4]), "+a"(acc[1][5]), "+a"(acc[1][6]), "+a"(acc[1][7]), "+a"(acc[2][0]), "+a"(acc[2][1]),          \
+    "+a"(acc[2][2]), "+a"(acc[2][3]), "+a"(acc[2][4]), "+a"(acc[2][5]), "+a"(acc[2][6]), "+a"(acc[2][7]),          \
+    "+a"(acc[3][0]), "+a"(acc[3][1]), "+a"(acc[3][2]), "+a"(acc[3][3]), "+a"(acc[3][4]), "+a"(acc[3][5]),          \
+    "+a"(acc[3][6]), "+a"(acc[3][7]), "+a"(acc[4][0]), "+a"(acc[4][1]), "+a"(acc[4][2]), "+a"(acc[4][3]),          \
+    "+a"(acc[4][4]), "+a"(acc[4][5]), "+a"(acc[4][6]), "+a"(acc[4][7]), "+a"(acc[5][0]), "+a"(acc[5][1]),          \
+    "+a"(acc[5][2]), "+a"(acc[5][3]), "+a"(acc[5][4]), "+a"(acc[5][5]), "+a"(acc[5][6]), "+a"(acc[5][7]),          \
+    "+a"(acc[6][0]), "+a"(acc[6][1]), "+a"(acc[6][2]), "+a"(acc[6][3]), "+a"(acc[6][4]), "+a"(acc[6][5]),          \
+    "+a"(acc[6][6]), "+a"(acc[6][7]), "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]),          \
+    "+a"(acc[7][4]), "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]),                                            \
+    "+v"(xf[0][0]), "+v"(xf[0][1]), "+v"(xf[0][2]), "+v"(xf[0][3]), "+v"(xf[0][4]), "+v"(xf[0][5]),                \
+    "+v"(xf[0][6]), "+v"(xf[0][7]), "+v"(wf[0][0]), "+v"(wf[0][1]), "+v"(wf[0][2]), "+v"(wf[0][3]),                \
+    "+v"(wf[0][4]), "+v"(wf[0][5]), "+v"(wf[0][6]), "+v"(wf[0][7]), "=&v"(xf[1][0]), "=&v"(xf[1][1]),                \
+    "=&v"(xf[1][2]), "=&v"(xf[1][3]), "=&v"(xf[1][4]), "=&v"(xf[1][5]), "=&v"(xf[1][6]), "=&v"(xf[1][7]),                \
+    "=&v"(wf[1][0]), "=&v"(wf[1][1]), "=&v"(wf[1][2]), "=&v"(wf[1][3]), "=&v"(wf[1][4]), "=&v"(wf[1][5]),                \
+    "=&v"(wf[1][6]), "=&v"(wf[1][7])                                                                                  \
+  : "v"(xb1[B_]), "v"(wb1[B_]), "v"(xb0[(B_) ^ 1]), "v"(wb0[(B_) ^ 1]), "v"(xo[0]), "v"(xo[1]), "v"(xo[2]),         \
+    "v"(xo[3]), "v"(xo[4]), "v"(xo[5]), "v"(xo[6]), "v"(xo[7]), "v"(wo[0]), "v"(wo[1]), "v"(wo[2]), "v"(wo[3]),     \
+    "v"(wo[4]), "v"(wo[5]), "v"(wo[6]), "v"(wo[7]), "s"(rx), "s"(rw), "s"(soff), "s"(mb[B_]), "s"(simd_odd)       \
+  : "memory", "m0", "scc"
+#define QZ_G16_ASM_PICK(SCH_, B_)                                                                                 \
+  do {                                                                                                             \
+    if constexpr (DT == QZ_DT_F16 && !kPerm) asm volatile(QZ_GEMM16_ASM_##SCH_##_NAT_F16 QZ_G16_ASM_OPS(B_));     \
+    else if constexpr (DT == QZ_DT_F16) asm volatile(QZ_GEMM16_ASM_##SCH_##_PERM_F16 QZ_G16_ASM_OPS(B_));        \
+    else if constexpr (!kPerm) asm volatile(QZ_GEMM16_ASM_##SCH_##_NAT_BF16 QZ_G16_ASM_OPS(B_));                  \
+    else asm volatile(QZ_GEMM16_ASM_##SCH_##_PERM_BF16 QZ_G16_ASM_OPS(B_));                                       \
+  } while (0)
+#define QZ_G16_ASM_LOOP(SCH_)                                                                                     \
+  do {                                                                                                             \
+    int s = 0;                                                                                                     \
+    for (; s + 1 < nsteps; s += 2) {                                                                               \
+      {                                                                                                            \
+        const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)min(s + 2, nsteps - 1) * (uint32_t)(kBK * 2)); \
+        QZ_G16_ASM_PICK(SCH_, 0);                                                                                  \
+      }                                                                                                            \
+      {                                                                                                            \
+        const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)min(s + 3, nsteps - 1) * (uint32_t)(kBK * 2)); \
+        QZ_G16_ASM_PICK(SCH_, 1);                                                                                  \
+      }                                                                                                            \
+    }                                                                                                              \
+    if (s < nsteps) {                                                                                              \
+      const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)min(s + 2, nsteps - 1) * (uint32_t)(kBK * 2)); \
+      QZ_G16_ASM_PICK(SCH_, 0);                                                                                    \
+    }                                                                                                              \
+  } while (0)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 is reserved: the compiler sets it before each of its own uses
+    if constexpr ((S & 128) != 0) QZ_G16_ASM_LOOP(DUAL);
+    else QZ_G16_ASM_LOOP(SPLIT);
+#pragma clang diagnostic pop
+#undef QZ_G16_ASM_LOOP
+#undef QZ_G16_ASM_PICK
+#undef QZ_G16_ASM_OPS
+  } else if constexpr ((S & 8) != 0) {
     // Rotated loop: an iteration runs MFMAs [kRot, 128) of step s and [0, kRot) of step s + 1, so
     // the loop header sits right after a lgkmcnt(0) + barrier -- the compiler's conservative wait at
     // a loop header then finds no LDS read outstanding (at the step boundary it waited for every
@@ -1690,6 +1768,203 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = v;
   }
   QZ_G16_STAMP(12);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_gemm16_4q: k_gemm16_4d<..., S = 64 | 2 (| 128)>'s hand-ordered asm step in a PERSISTENT
+// workgroup (one per CU, as the library's MT256x256x64 kernel runs) that walks tiles id, id + grid,
+// ... in the grouped XCD-aware order.  A tile's last two steps stage the NEXT tile's steps 0 and 1,
+// so the k-half 0 fragments of its first step are in registers when the tile ends; the epilogue
+// stores the permuted accumulators straight from the registers (no LDS, no barrier) and the next
+// tile's first step starts its k-half 0 MFMAs from 0 (*_FIRST) instead of zeroing 256 AGPRs.  Same
+// MFMAs in the same order per output as k_gemm16_4d: bit-identical.  Host contract: nsteps = K / 64
+// even (every tile starts on buffer 0), grid <= tiles.  S & 128: DUAL (the library's two event
+// orders by SIMD parity), else SPLIT.
+struct Gemm4qOffs {
+  uint32_t x[8], w[8];
+};
+template <int DT, int S>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_gemm16_4q(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * k4dBuf];
+  typedef __attribute__((address_space(3))) void *lds_ptr_t;
+  typedef __attribute__((address_space(3))) unsigned char lds_uc;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wt = wave >> 1, wm = wave & 1;
+  const int tiles_m = (p.M + k4wM - 1) / k4wM, tiles_t = (p.T + k4wT - 1) / k4wT;
+  const int ntiles = tiles_m * tiles_t;
+  const int nsteps = p.K / kBK;
+  auto tile_of = [&](int id, int &m0, int &t0) {
+    const int q8 = ntiles >> 3, r8 = ntiles & 7, xcd = id & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+    int tm = wg % tiles_m, tt = wg / tiles_m;
+    if (tiles_m % 8 == 0 && tiles_t % 4 == 0) {
+      const int grp = wg / (4 * tiles_m), r = wg % (4 * tiles_m);
+      tt = 4 * grp + (r % 32) / 8;
+      tm = 8 * (r / 32) + r % 8;
+    }
+    m0 = tm * k4wM;
+    t0 = tt * k4wT;
+  };
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void *>(p.X), (short)0, (int)((uint32_t)p.T * (uint32_t)p.ldx * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char *>(p.B), (short)0, (int)((uint32_t)p.M * (uint32_t)p.K * 2u), 0x00020000);
+  // k_gemm16_4d's DMA pieces and swizzles (X: chunk ^ row bits 1..3; W: the S & 2 one)
+  const int wr = tid >> 3;
+  const uint32_t sw = (uint32_t)((tid & 7) ^ ((tid >> 4) & 7));
+  const uint32_t sww = (uint32_t)((tid & 7) ^ (((wr >> 1) & 1) | (((wr >> 3) & 1) << 1) | (((wr >> 4) & 1) << 2)));
+  auto offs_of = [&](int m0, int t0, Gemm4qOffs &o) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int row = 32 * c + wr;
+      o.x[c] = ((uint32_t)min(t0 + row, p.T - 1) * (uint32_t)p.ldx + 8u * sw) * 2u;
+      o.w[c] = ((uint32_t)min(m0 + row, p.M - 1) * (uint32_t)p.K + 8u * sww) * 2u;
+    }
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const uint32_t fl[2] = {(uint32_t)(fr * 128 + ((fk ^ ((fr >> 1) & 7)) << 4)),
+                          (uint32_t)(fr * 128 + (((fk ^ ((fr >> 1) & 7)) ^ 4) << 4))};
+  const int fwz = ((fr >> 1) & 1) | (((fr >> 2) & 1) << 1) | (((fr >> 3) & 1) << 2);
+  const uint32_t wl[2] = {(uint32_t)((8 * (fr >> 2) + (fr & 3)) * 128 + ((fk ^ fwz) << 4)),
+                          (uint32_t)((8 * (fr >> 2) + (fr & 3)) * 128 + (((fk ^ fwz) ^ 4) << 4))};
+  v4u xf[2][8], wf[2][8];
+  f4_t acc[8][8];
+  const uint32_t sb = (uint32_t)(uintptr_t)(lds_uc *)smem;
+  const uint32_t simd_odd = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_s_getreg((0 << 11) | (4 << 6) | 4) & 1);
+  uint32_t xb1[2], wb1[2], xb0[2], wb0[2], mb[2];
+#pragma unroll
+  for (int buf = 0; buf < 2; ++buf) {
+    const uint32_t bb = sb + (uint32_t)(buf * k4dBuf);
+    xb1[buf] = bb + fl[1] + (uint32_t)(128 * wt) * 128u;
+    xb0[buf] = bb + fl[0] + (uint32_t)(128 * wt) * 128u;
+    wb1[buf] = bb + (uint32_t)k4wStage + wl[1] + (uint32_t)(128 * wm) * 128u;
+    wb0[buf] = bb + (uint32_t)k4wStage + wl[0] + (uint32_t)(128 * wm) * 128u;
+    mb[buf] = __builtin_amdgcn_readfirstlane(bb + 1024u * (uint32_t)wave);
+  }
+
+  int id = blockIdx.x;
+  if (id >= ntiles) return;
+  int m0, t0, nm0 = 0, nt0 = 0;
+  tile_of(id, m0, t0);
+  Gemm4qOffs cur, nxt;
+  offs_of(m0, t0, cur);
+  // ---- first tile: steps 0 and 1 in flight, step 0's k-half 0 in registers ----
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    unsigned char *d = smem + 4096 * c + 1024 * wave;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)d, 16, cur.x[c], 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(d + k4wStage), 16, cur.w[c], 0, 0, 0);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    unsigned char *d = smem + k4dBuf + 4096 * c + 1024 * wave;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)d, 16, cur.x[c], kBK * 2, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(d + k4wStage), 16, cur.w[c], kBK * 2, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    xf[0][i] = *reinterpret_cast<const v4u *>(smem + fl[0] + (128 * wt + 16 * i) * 128);
+    wf[0][i] = *reinterpret_cast<const v4u *>(smem + k4wStage + wl[0] + (128 * wm + 32 * (i >> 1) + 4 * (i & 1)) * 128);
+  }
+
+  // A_: "+a" for a step that accumulates, "=a" for a tile's first (*_FIRST: the previous tile's
+  // sums are dead once stored, so nothing carries the accumulators across the epilogue).  The k-half 1
+  // fragments are written (early, while the inputs are still read) before a step uses them: "=&v",
+  // so they are dead between steps; the k-half 0 ones carry over to the next step: "+v".
+#define QZ_G16Q_OPS(B_, O_, A_)                                                                                       \
+  : A_(acc[0][0]), A_(acc[0][1]), A_(acc[0][2]), A_(acc[0][3]), A_(acc[0][4]), A_(acc[0][5]),          \
+    A_(acc[0][6]), A_(acc[0][7]), A_(acc[1][0]), A_(acc[1][1]), A_(acc[1][2]), A_(acc[1][3]),          \
+    A_(acc[1][4]), A_(acc[1][5]), A_(acc[1][6]), A_(acc[1][7]), A_(acc[2][0]), A_(acc[2][1]),          \
+    A_(acc[2][2]), A_(acc[2][3]), A_(acc[2][4]), A_(acc[2][5]), A_(acc[2][6]), A_(acc[2][7]),          \
+    A_(acc[3][0]), A_(acc[3][1]), A_(acc[3][2]), A_(acc[3][3]), A_(acc[3][4]), A_(acc[3][5]),          \
+    A_(acc[3][6]), A_(acc[3][7]), A_(acc[4][0]), A_(acc[4][1]), A_(acc[4][2]), A_(acc[4][3]),          \
+    A_(acc[4][4]), A_(acc[4][5]), A_(acc[4][6]), A_(acc[4][7]), A_(acc[5][0]), A_(acc[5][1]),          \
+    A_(acc[5][2]), A_(acc[5][3]), A_(acc[5][4]), A_(acc[5][5]), A_(acc[5][6]), A_(acc[5][7]),          \
+    A_(acc[6][0]), A_(acc[6][1]), A_(acc[6][2]), A_(acc[6][3]), A_(acc[6][4]), A_(acc[6][5]),          \
+    A_(acc[6][6]), A_(acc[6][7]), A_(acc[7][0]), A_(acc[7][1]), A_(acc[7][2]), A_(acc[7][3]),          \
+    A_(acc[7][4]), A_(acc[7][5]), A_(acc[7][6]), A_(acc[7][7]),                                            \
+    "+v"(xf[0][0]), "+v"(xf[0][1]), "+v"(xf[0][2]), "+v"(xf[0][3]), "+v"(xf[0][4]), "+v"(xf[0][5]),                \
+    "+v"(xf[0][6]), "+v"(xf[0][7]), "+v"(wf[0][0]), "+v"(wf[0][1]), "+v"(wf[0][2]), "+v"(wf[0][3]),                \
+    "+v"(wf[0][4]), "+v"(wf[0][5]), "+v"(wf[0][6]), "+v"(wf[0][7]), "=&v"(xf[1][0]), "=&v"(xf[1][1]),                \
+    "=&v"(xf[1][2]), "=&v"(xf[1][3]), "=&v"(xf[1][4]), "=&v"(xf[1][5]), "=&v"(xf[1][6]), "=&v"(xf[1][7]),                \
+    "=&v"(wf[1][0]), "=&v"(wf[1][1]), "=&v"(wf[1][2]), "=&v"(wf[1][3]), "=&v"(wf[1][4]), "=&v"(wf[1][5]),                \
+    "=&v"(wf[1][6]), "=&v"(wf[1][7])                                                                                  \
+  : "v"(xb1[B_]), "v"(wb1[B_]), "v"(xb0[(B_) ^ 1]), "v"(wb0[(B_) ^ 1]), "v"(O_.x[0]), "v"(O_.x[1]), "v"(O_.x[2]),   \
+    "v"(O_.x[3]), "v"(O_.x[4]), "v"(O_.x[5]), "v"(O_.x[6]), "v"(O_.x[7]), "v"(O_.w[0]), "v"(O_.w[1]), "v"(O_.w[2]), \
+    "v"(O_.w[3]), "v"(O_.w[4]), "v"(O_.w[5]), "v"(O_.w[6]), "v"(O_.w[7]), "s"(rx), "s"(rw), "s"(soff), "s"(mb[B_]),  \
+    "s"(simd_odd)                                                                                                   \
+  : "memory", "m0", "scc"
+  // one step on buffer B_ whose DMAs fetch step DS_ of the tile O_ describes
+#define QZ_G16Q_STEP(SCH_, B_, O_, DS_, A_)                                                                       \
+  do {                                                                                                             \
+    const uint32_t soff = __builtin_amdgcn_readfirstlane((uint32_t)(DS_) * (uint32_t)(kBK * 2));                  \
+    if constexpr (DT == QZ_DT_F16) asm volatile(QZ_GEMM16_ASM_##SCH_##_F16 QZ_G16Q_OPS(B_, O_, A_));              \
+    else asm volatile(QZ_GEMM16_ASM_##SCH_##_BF16 QZ_G16Q_OPS(B_, O_, A_));                                       \
+  } while (0)
+  // a tile: step 0 from zero, steps 1 .. nsteps - 3 staging this tile's steps + 2, the last two
+  // staging the next tile's steps 0 and 1
+#define QZ_G16Q_TILE(SCH_)                                                                                        \
+  do {                                                                                                             \
+    if (nsteps > 2) {                                                                                              \
+      QZ_G16Q_STEP(SCH_##_PERM_FIRST, 0, cur, 2, "=a");                                                                  \
+      QZ_G16Q_STEP(SCH_##_PERM, 1, cur, 3, "+a");                                                                        \
+      for (int s = 2; s + 2 < nsteps; s += 2) {                                                                    \
+        QZ_G16Q_STEP(SCH_##_PERM, 0, cur, s + 2, "+a");                                                                  \
+        QZ_G16Q_STEP(SCH_##_PERM, 1, cur, s + 3, "+a");                                                                  \
+      }                                                                                                            \
+      QZ_G16Q_STEP(SCH_##_PERM, 0, nxt, 0, "+a");                                                                        \
+    } else {                                                                                                       \
+      QZ_G16Q_STEP(SCH_##_PERM_FIRST, 0, nxt, 0, "=a");                                                                  \
+    }                                                                                                              \
+    QZ_G16Q_STEP(SCH_##_PERM, 1, nxt, 1, "+a");                                                                          \
+  } while (0)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 is reserved: the compiler sets it before each of its own uses
+  for (;;) {
+    const int nid = id + (int)gridDim.x;
+    const bool more = nid < ntiles;
+    if (more) {
+      tile_of(nid, nm0, nt0);
+      offs_of(nm0, nt0, nxt);
+    } else {
+      nxt = cur;  // clamped copies of this tile's steps 0 and 1 into buffers nobody reads again
+    }
+    if constexpr ((S & 128) != 0) QZ_G16Q_TILE(DUAL);
+    else QZ_G16Q_TILE(SPLIT);
+    // the MFMA results' read-after-write wait before the accumulators are read (the asm's own
+    // tail covers most of it)
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    // ---- epilogue straight from the accumulators (k_gemm16_4d's S & 2 one): 16-B stores of 8
+    // consecutive rows; the next tile's first step overwrites the accumulators ----
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int m = m0 + 128 * wm + 32 * J + 8 * fk;
+      float bv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bv[r] = p.bias ? load_f32<DT>(p.bias, min(m + r, p.M - 1)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int t = t0 + 128 * wt + 16 * i + fr;
+        const f4_t lo = acc[2 * J][i], hi = acc[2 * J + 1][i];
+        const v4u o = v4u{cvt_pk16<DT>(lo[0] + bv[0], lo[1] + bv[1]), cvt_pk16<DT>(lo[2] + bv[2], lo[3] + bv[3]),
+                          cvt_pk16<DT>(hi[0] + bv[4], hi[1] + bv[5]), cvt_pk16<DT>(hi[2] + bv[6], hi[3] + bv[7])};
+        if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = o;
+      }
+    }
+    if (!more) break;
+    id = nid;
+    m0 = nm0;
+    t0 = nt0;
+    cur = nxt;
+  }
+#pragma clang diagnostic pop
+#undef QZ_G16Q_TILE
+#undef QZ_G16Q_STEP
+#undef QZ_G16Q_OPS
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): the clamped DMAs land before the workgroup ends
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2088,7 +2363,8 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 // QZ_GEMM16_SCHED (read once at load, reported and set through qz_gemv_knobs / qz_gemv_set_knob):
 // the k_gemm16_4d schedule qz_gemm_16bit launches -- 0: P1/P2 segments; S bits: 1 split-release
 // schedule, 2 permuted W rows + 16-B register epilogue, 8 the split schedule's loop rotated, 16 (with 8)
-// the waves on odd SIMDs run the schedule one MFMA later
+// the waves on odd SIMDs run the schedule one MFMA later, 64 (with 1) each step one hand-ordered asm
+// stream (gemm16_asm_step.h), 128 (with 64) the library's two event orders by SIMD parity
 namespace qz {
 int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
 }
@@ -2117,9 +2393,24 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   p.k_split = K;
   const unsigned g = (unsigned)(((M + k4wM - 1) / k4wM) * ((T + k4wT - 1) / k4wT));
   hipStream_t s = (hipStream_t)stream;
+  const int sched = gemm16_sched();
+  // S & 512: the persistent form (k_gemm16_4q), one workgroup per CU, when every tile starts on
+  // buffer 0 (K / 64 even); otherwise the schedule's non-persistent kernel
+  if ((sched & 512) != 0 && (K / kBK) % 2 == 0) {
+    const unsigned gq = std::min(g, (unsigned)device_cus());
+#define QZ_G16Q(DT_, S_) hipLaunchKernelGGL((k_gemm16_4q<DT_, S_>), dim3(gq), dim3(256), 0, s, p)
+    if (dtype == QZ_DT_F16) {
+      if (sched & 128) QZ_G16Q(QZ_DT_F16, 128); else QZ_G16Q(QZ_DT_F16, 0);
+    } else {
+      if (sched & 128) QZ_G16Q(QZ_DT_BF16, 128); else QZ_G16Q(QZ_DT_BF16, 0);
+    }
+#undef QZ_G16Q
+    QZ_LAUNCH_CHECK();
+    return QZ_OK;
+  }
 #define QZ_G16(DT_, S_) hipLaunchKernelGGL((k_gemm16_4d<DT_, 64, 16, 112, S_>), dim3(g), dim3(256), 0, s, p)
 #define QZ_G16S(DT_)                   \
-  switch (gemm16_sched()) {            \
+  switch (sched & 511) {               \
     case 1: QZ_G16(DT_, 1); break;     \
     case 2: QZ_G16(DT_, 2); break;     \
     case 3: QZ_G16(DT_, 3); break;     \
@@ -2127,6 +2418,10 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
     case 11: QZ_G16(DT_, 11); break;   \
     case 25: QZ_G16(DT_, 25); break;   \
     case 27: QZ_G16(DT_, 27); break;   \
+    case 65: QZ_G16(DT_, 65); break;   \
+    case 67: QZ_G16(DT_, 67); break;   \
+    case 193: QZ_G16(DT_, 193); break; \
+    case 195: QZ_G16(DT_, 195); break; \
     default: QZ_G16(DT_, 0); break;    \
   }
   if (dtype == QZ_DT_F16) {

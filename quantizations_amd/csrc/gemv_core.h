@@ -982,20 +982,6 @@ constexpr size_t kLdsPerCU = 160 * 1024;   // gfx950: LDS per compute unit
 // the knobs the library read at load (gemv.hip); qz_gemv_set_knob changes one explicitly
 Knobs &gemv_knobs();
 
-// Compute units of the current device (hipDeviceGetAttribute), cached per device: the persistent
-// grids are sized in workgroups per CU.
-static int device_cus() {
-  static std::atomic<int> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  int v = cache[dev].load(std::memory_order_relaxed);
-  if (v <= 0) {
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cache[dev].store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
 static int ilog2(long long v) {
   int l = 0;
   while ((1LL << l) < v) ++l;

@@ -41,7 +41,8 @@ int main(int argc, char **argv) {
   struct V { std::string n; std::function<void()> f; std::vector<double> us; unsigned long long st[8 * 4 * 16]; };
   std::vector<V> vs;
 #define ADD(SK_, S_) vs.push_back({"SK=" #SK_ " S=" #S_, [=]() { hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, SK_, 16, 112, S_>), dim3(g), dim3(256), 0, 0, p); }, {}, {}})
-  ADD(64, 0); ADD(64, 1); ADD(64, 3); ADD(64, 9); ADD(64, 11); ADD(64, 25); ADD(64, 27); ADD(65, 0); ADD(65, 9); ADD(65, 25);
+#define ADDQ(S_) vs.push_back({"4q S=" #S_, [=]() { hipLaunchKernelGGL((k_gemm16_4q<QZ_DT_F16, S_>), dim3(std::min(g, 256u)), dim3(256), 0, 0, p); }, {}, {}})
+  ADD(64, 0); ADD(64, 65); ADD(64, 67); ADD(64, 195); ADD(65, 0); ADDQ(0); ADDQ(128);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());

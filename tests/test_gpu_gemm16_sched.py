@@ -1,5 +1,5 @@
 """GPU: every k_gemm16_4d schedule qz_gemm_16bit can launch (QZ_GEMM16_SCHED: the split-release
-step schedule, the permuted-W-row register epilogue, the unstaged last steps) gives the SAME bits as
+step schedule, the permuted-W-row register epilogue, the unstaged last steps, the asm step, the persistent form) gives the SAME bits as
 schedule 0, which test_gpu_edges.py checks against fp64 of the bit-exact dequantised weight (each
 output element sums its k products in the same order under every schedule; only the issue order of
 the LDS reads / DMAs and the epilogue path differ).  Ragged T and M tiles, 1-4-step K loops, bias,
@@ -10,7 +10,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda")
-SCHEDS = [1, 2, 3, 9, 11, 25, 27]
+# 512 |: the persistent k_gemm16_4q (one workgroup per CU, the next tile's steps 0 / 1 staged by the
+# last two steps of a tile) where K / 64 is even, else the non-persistent schedule
+SCHEDS = [1, 2, 3, 9, 11, 25, 27, 65, 67, 193, 195, 579, 707]
 
 
 @pytest.fixture
@@ -23,7 +25,9 @@ def sched_knob():
 
 
 @pytest.mark.parametrize("T,M,K", [(4096, 1024, 4096), (4100, 1032, 256), (300, 264, 192), (37, 264, 64),
-                                   (257, 1032, 128), (1, 8, 64), (512, 520, 4160)])
+                                   (257, 1032, 128), (1, 8, 64), (512, 520, 4160),
+                                   # > 256 tiles: persistent workgroups walk 2 tiles (grouped order; ragged)
+                                   (8192, 4096, 128), (4100, 4104, 256)])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("bias", [False, True])
 def test_gemm16_schedules_bit_identical(sched_knob, T, M, K, dtype, bias):

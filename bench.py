@@ -835,7 +835,7 @@ def prefill_bench(T: int = 16384, iters: int = 10):
                     f"MFMA kernels up to {fused_max_tokens(4096)} tokens ({fused_max_tokens(1024)} for 1024 or "
                     f"14336 rows), above it our dequant kernel + hipBLASLt "
                     "(the reference's F.linear route) unless QZ_PREFILL_GEMM16=1 selects our 4-wave LDS-DMA MFMA GEMM "
-                    f"(qz_gemm_16bit, >= {GEMM16_MIN_TILES} 256x256 tiles)"}
+                    f"(qz_gemm_16bit: the persistent k_gemm16_4q, >= {GEMM16_MIN_TILES} 256x256 tiles)"}
 
 
 @torch.inference_mode()

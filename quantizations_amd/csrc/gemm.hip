@@ -2364,7 +2364,8 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 // the k_gemm16_4d schedule qz_gemm_16bit launches -- 0: P1/P2 segments; S bits: 1 split-release
 // schedule, 2 permuted W rows + 16-B register epilogue, 8 the split schedule's loop rotated, 16 (with 8)
 // the waves on odd SIMDs run the schedule one MFMA later, 64 (with 1) each step one hand-ordered asm
-// stream (gemm16_asm_step.h), 128 (with 64) the library's two event orders by SIMD parity
+// stream (gemm16_asm_step.h), 128 (with 64) the library's two event orders by SIMD parity, 512 (with
+// 64 | 2) the persistent k_gemm16_4q where K / 64 is even.  Default 707 = 512 | 128 | 64 | 2 | 1
 namespace qz {
 int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
 }

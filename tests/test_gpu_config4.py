@@ -8,7 +8,9 @@ for bit in test_gpu_parity; the oracle itself is too slow for 2e14 FLOP):
   * Linear4bit.forward in its default (auto) mode, i.e. modules.py:62-64's
     `F.linear(A, dequantize_4bit(W).t())` as the product routes it;
   * gemm_4bit(route="fused"): the hand-written MFMA kernel (256 x 256 tile at
-    T >= 4096, 128-row tile below).
+    T >= 4096, 128-row tile below);
+  * gemm_4bit(route="gemm16"): the bit-exact dequant, then qz_gemm_16bit (its default
+    schedule, the persistent k_gemm16_4q) -- the hand-written replacement for the library GEMM.
 Bar: ||y - y_ref|| / ||y_ref|| <= 1e-3 and |y - y_ref| <= 1e-3 max|y_ref| + 1 ulp
 (fp16), as everywhere else.
 """
@@ -58,6 +60,10 @@ def test_config4_prefill_T16384_both_routes(M, K):
     y_fused = gemm_4bit(X, m.weight, m.weight.quant_state, route="fused")   # 256 x 256 MFMA tile kernel
     assert y_fused.shape == (8, 2048, M)
     _assert_close_dev(y_fused.reshape(-1, M), ref, f"fused {M}x{K}")
+    del y_fused
+    y16 = gemm_4bit(X, m.weight, m.weight.quant_state, route="gemm16")   # dequant + k_gemm16_4q
+    assert y16.shape == (8, 2048, M)
+    _assert_close_dev(y16.reshape(-1, M), ref, f"gemm16 {M}x{K}")
 
 
 @pytest.mark.parametrize("T", [513, 2048])

@@ -19,7 +19,7 @@ SCHEDS = [1, 2, 3, 9, 11, 25, 27, 65, 67, 193, 195, 579, 707]
 def sched_knob():
     from quantizations_amd import _lib
 
-    before = _lib.gemv_knobs().get("QZ_GEMM16_SCHED", 0)
+    before = _lib.gemv_knobs().get("QZ_GEMM16_SCHED", 707)
     yield lambda s: _lib.set_gemv_knob("QZ_GEMM16_SCHED", s)
     _lib.set_gemv_knob("QZ_GEMM16_SCHED", before)
 

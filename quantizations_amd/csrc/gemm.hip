@@ -1932,7 +1932,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     } else {
       nxt = cur;  // clamped copies of this tile's steps 0 and 1 into buffers nobody reads again
     }
-    if constexpr ((S & 128) != 0) QZ_G16Q_TILE(DUAL);
+    if constexpr ((S & 256) != 0) QZ_G16Q_TILE(DUALW);   // W's k-half 1 reads and refill first
+    else if constexpr ((S & 128) != 0) QZ_G16Q_TILE(DUAL);
     else QZ_G16Q_TILE(SPLIT);
     // the MFMA results' read-after-write wait before the accumulators are read (the asm's own
     // tail covers most of it)
@@ -2365,7 +2366,8 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 // schedule, 2 permuted W rows + 16-B register epilogue, 8 the split schedule's loop rotated, 16 (with 8)
 // the waves on odd SIMDs run the schedule one MFMA later, 64 (with 1) each step one hand-ordered asm
 // stream (gemm16_asm_step.h), 128 (with 64) the library's two event orders by SIMD parity, 512 (with
-// 64 | 2) the persistent k_gemm16_4q where K / 64 is even.  Default 707 = 512 | 128 | 64 | 2 | 1
+// 64 | 2) the persistent k_gemm16_4q where K / 64 is even, 256 (with 512) W's k-half 1 fragments
+// read and its image refilled before X's.  Default 963 = 512 | 256 | 128 | 64 | 2 | 1
 namespace qz {
 int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
 }
@@ -2401,9 +2403,13 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
     const unsigned gq = std::min(g, (unsigned)device_cus());
 #define QZ_G16Q(DT_, S_) hipLaunchKernelGGL((k_gemm16_4q<DT_, S_>), dim3(gq), dim3(256), 0, s, p)
     if (dtype == QZ_DT_F16) {
-      if (sched & 128) QZ_G16Q(QZ_DT_F16, 128); else QZ_G16Q(QZ_DT_F16, 0);
+      if (sched & 256) QZ_G16Q(QZ_DT_F16, 384);
+      else if (sched & 128) QZ_G16Q(QZ_DT_F16, 128);
+      else QZ_G16Q(QZ_DT_F16, 0);
     } else {
-      if (sched & 128) QZ_G16Q(QZ_DT_BF16, 128); else QZ_G16Q(QZ_DT_BF16, 0);
+      if (sched & 256) QZ_G16Q(QZ_DT_BF16, 384);
+      else if (sched & 128) QZ_G16Q(QZ_DT_BF16, 128);
+      else QZ_G16Q(QZ_DT_BF16, 0);
     }
 #undef QZ_G16Q
     QZ_LAUNCH_CHECK();
@@ -2411,7 +2417,7 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   }
 #define QZ_G16(DT_, S_) hipLaunchKernelGGL((k_gemm16_4d<DT_, 64, 16, 112, S_>), dim3(g), dim3(256), 0, s, p)
 #define QZ_G16S(DT_)                   \
-  switch (sched & 511) {               \
+  switch (sched & 255) {               \
     case 1: QZ_G16(DT_, 1); break;     \
     case 2: QZ_G16(DT_, 2); break;     \
     case 3: QZ_G16(DT_, 3); break;     \

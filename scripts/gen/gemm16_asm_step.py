@@ -48,6 +48,7 @@ SCHEDS = {
                 [(21, "lgkm"), (22, "bar"), (51, "lgkm"), (52, "bar"), (92, "vm13"), (93, "bar"), (127, "lgkm")]),
 }
 DMAS = [("dx", c) for c in range(8)] + [("dw", c) for c in range(8)]   # issue order
+DMAS_WF = [("dw", c) for c in range(8)] + [("dx", c) for c in range(8)]
 
 
 def m0_for(kind, c):
@@ -58,11 +59,20 @@ def w_off(j, perm):
     return (4096 * (j >> 1) + 512 * (j & 1)) if perm else 2048 * j
 
 
-def stream(ev, perm, t, first=False):
+def wfirst(ev):
+    """The same slots with the operands' k-half 1 reads and refill DMAs swapped: W's fragments read
+    first, so the W image is released (and refilled) first, X's after the second wait."""
+    sw = {"rx1": "rw1", "rw1": "rx1", "dx": "dw", "dw": "dx"}
+    return {c: [(sw.get(k, k), i) for k, i in es] for c, es in ev.items()}
+
+
+def stream(ev, perm, t, first=False, dmas=None):
+    DMAS = dmas or globals()["DMAS"]
     order = sorted((c, e) for c, es in ev.items() for e in es if e[0] in ("dx", "dw"))
     assert [e for _, e in order] == DMAS, order
     dmacount = sum(1 for c, es in ev.items() for e in es if e[0] in ("dx", "dw") and c < 92)
-    assert dmacount == 13, dmacount
+    vmw = [e[0] for es in ev.values() for e in es if e[0] in ("vm13", "vm16")]
+    assert dmacount == (16 if vmw == ["vm16"] else 13), (dmacount, vmw)
     out = [f"s_add_u32 m0, %119, {m0_for(*DMAS[0])}"]
     d = 0
     for n in range(128):
@@ -72,8 +82,8 @@ def stream(ev, perm, t, first=False):
         b = 64 + i if kk == 0 else 80 + i         # X fragment operand
         # first: a tile's step 0 -- the k-half 0 MFMAs start from 0, not from the accumulator
         out.append(f"v_mfma_f32_16x16x32_{t} %{m}, %{a}, %{b}, {0 if first and kk == 0 else '%' + str(m)}")
-        for kind, idx in sorted(ev.get(n + 1, []), key=lambda e: ("lgkm", "vm13", "bar").index(e[0])
-                                if e[0] in ("lgkm", "vm13", "bar") else -1):
+        for kind, idx in sorted(ev.get(n + 1, []), key=lambda e: ("lgkm", "vm13", "vm16", "bar").index(e[0])
+                                if e[0] in ("lgkm", "vm13", "vm16", "bar") else -1):
             if kind == "rx1":
                 out.append(f"ds_read_b128 %{80 + idx}, %96 offset:{2048 * idx}")
             elif kind == "rw1":
@@ -94,6 +104,8 @@ def stream(ev, perm, t, first=False):
                 out.append("s_waitcnt lgkmcnt(0)")
             elif kind == "vm13":
                 out.append("s_waitcnt vmcnt(13)")
+            elif kind == "vm16":
+                out.append("s_waitcnt vmcnt(16)")
             elif kind == "bar":
                 out.append("s_barrier")
     assert d == 16
@@ -120,6 +132,17 @@ for perm in (False, True):
             for ln in body:
                 print(f'  "{ln}\\n\\t" \\')
             print('  ""')
+for t in ("f16", "bf16"):
+    for first in (False, True):
+        w = 'PERM' + ('_FIRST' if first else '')
+        print(f"#define QZ_GEMM16_ASM_DUALW_{w}_{t.upper()} \\")
+        body = (["s_cmp_lg_u32 %120, 0", "s_cbranch_scc1 .Lqz_g16_l1_%=",]
+                + stream(wfirst(SCHEDS["L0"]), True, t, first, DMAS_WF)
+                + ["s_branch .Lqz_g16_end_%=", ".Lqz_g16_l1_%=:"]
+                + stream(wfirst(SCHEDS["L1"]), True, t, first, DMAS_WF) + [".Lqz_g16_end_%=:"])
+        for ln in body:
+            print(f'  "{ln}\\n\\t" \\')
+        print('  ""')
 for t in ("f16", "bf16"):
     print(f"#define QZ_GEMM16_ASM_SPLIT_PERM_FIRST_{t.upper()} \\")
     for ln in stream(SCHEDS["SPLIT"], True, t, True):

@@ -207,7 +207,7 @@ __device__ unsigned long long *g_qz_stamp;
 #define QZ_STAMP_DECL unsigned long long qz_st_[6] = {0, 0, 0, 0, 0, 0}
 #define QZ_STAMP(k)                                                                  \
   do {                                                                               \
-    if constexpr (STAMP != 0 && (STAMP == 1 || (k) == 0 || (k) == 4)) {              \
+    if constexpr ((STAMP & 3) != 0 && ((STAMP & 3) == 1 || (k) == 0 || (k) == 4)) {  \
       __builtin_amdgcn_sched_barrier(0);                                             \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(qz_st_[k])::"memory"); \
       __builtin_amdgcn_sched_barrier(0);                                             \
@@ -215,13 +215,13 @@ __device__ unsigned long long *g_qz_stamp;
   } while (0)
 #define QZ_STAMP_FLUSH(wave_id)                                                      \
   do {                                                                               \
-    if constexpr (STAMP != 0) {                                                      \
+    if constexpr ((STAMP & 3) != 0) {                                                \
       uint32_t xcc, hw;                                                              \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));             \
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));               \
       qz_st_[5] = ((unsigned long long)xcc << 32) | hw;                              \
       if ((threadIdx.x & 63) == 0) {                                                 \
-        if constexpr (STAMP == 2) {                                                  \
+        if constexpr ((STAMP & 3) == 2) {                                            \
           g_qz_stamp[(size_t)(wave_id) * 8 + 0] = qz_st_[0];                         \
           g_qz_stamp[(size_t)(wave_id) * 8 + 4] = qz_st_[4];                         \
         } else {                                                                     \
@@ -703,13 +703,15 @@ __device__ __forceinline__ void gemv_body(const GemvParams &p_in, const int bloc
       const int S = lut_shift(p.lut);
       out_scale = ldexpf(1.0f, -S);
       build_byte_table_exact<NW * 64, kPieces>(s_tab, p.lut, S);
-    } else if (threadIdx.x < 256) {
+    } else if (threadIdx.x < 256 && (STAMP & 48) == 0) {
       store_byte_table_entry<kPieces>(s_tab, tab_entry);
     }
   } else if (threadIdx.x < 256) {   // fp16 codes: the built-in books only (a runtime book is exact)
     store_byte_table_entry<kPieces>(s_tab, tab_entry);
   }
-  __syncthreads();
+  // STAMP & 16 / 32 (microbenchmark ablations, wrong results): no byte-table stores / also no
+  // prologue barrier
+  if constexpr ((STAMP & 32) == 0) __syncthreads();
   if constexpr (NRM) {  // rs as k_rmsnorm (torch MeanOps: sum * (1/N), then rsqrt(var + eps)); x' -> LDS
     const float tot = __fadd_rn(__fadd_rn(s_nss[0], s_nss[1]), __fadd_rn(s_nss[2], s_nss[3]));
     const float rs = rsqrtf(__fadd_rn(__fmul_rn(tot, 1.0f / (float)p.K), p.eps));

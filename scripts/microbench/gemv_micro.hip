@@ -106,7 +106,18 @@ int main(int argc, char **argv) {
     q.tabsel = (CL_) ? 2 : 0; q.out_scale = (CL_) ? 1.0f / 16384 : 1.0f; \
     const unsigned g = (unsigned)((M + R * (NW / WK) - 1) / (R * (NW / WK))); \
     hipLaunchKernelGGL((k_gemv_4bit<true, QZ_DT_F16, R, WK, NW, true, CL_, WT_, TWO_>), dim3(g), dim3(NW * 64), 0, 0, q); })
+#define GVA(R, NW, ABL) timeit("gemv R=" #R " NW=" #NW " CL TWO abl=" #ABL, \
+    [&, pt = p](int i) { \
+    GemvParams q = pt; q.B = P[i % NC]; q.sc.qabsmax = Q[i % NC]; q.sc.absmax2 = A2[i % NC]; \
+    q.tabsel = 2; q.out_scale = 1.0f / 16384; \
+    const unsigned g = (unsigned)((M + R * NW - 1) / (R * NW)); \
+    hipLaunchKernelGGL((k_gemv_4bit<true, QZ_DT_F16, R, 1, NW, true, true, false, true, ABL>), dim3(g), dim3(NW * 64), 0, 0, q); })
   const bool two = K == 4096;
+  if (mode == "abl") {  // K = 4096 only: the prologue's table stores (16) and barrier (32) ablated (wrong results)
+    GVA(2, 4, 0); GVA(2, 4, 16); GVA(2, 4, 48);
+    GV(2, 1, 4, true, true, true); GV(2, 1, 8, true, true, true); GV(1, 1, 8, true, true, true);
+    GV(4, 1, 8, true, true, true); GV(1, 1, 4, true, false, true);
+  }
   if (mode == "geom") {
     if (two) {
       GV(2, 1, 4, true, false, true); GV(2, 1, 4, false, false, true); GV(4, 1, 4, true, false, true);

@@ -118,6 +118,10 @@ int main(int argc, char **argv) {
     GV(2, 1, 4, true, true, true); GV(2, 1, 8, true, true, true); GV(1, 1, 8, true, true, true);
     GV(4, 1, 8, true, true, true); GV(1, 1, 4, true, false, true);
   }
+  if (mode == "nw16") {  // 16-wave workgroups sharing one wide table (4 waves per SIMD) vs the product's 8
+    GV(2, 1, 8, true, true, false); GV(1, 1, 16, true, true, false); GV(2, 1, 16, true, true, false);
+    GV(1, 1, 8, true, true, false); GV(4, 1, 16, true, true, false);
+  }
   if (mode == "geom") {
     if (two) {
       GV(2, 1, 4, true, false, true); GV(2, 1, 4, false, false, true); GV(4, 1, 4, true, false, true);

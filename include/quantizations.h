@@ -367,7 +367,7 @@ int qz_gemv_4bit_pair_silu(const qz_gemv_segment *segs, int K, const void *x, in
                            void *h, void *stream);
 
 /* The launch-geometry measurement knobs in effect (QZ_GEMV_WIDE8, QZ_GROUPED_NORM_R, QZ_PAIR_R,
- * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1, and QZ_GEMM16_SCHED -- the schedule qz_gemm_16bit (default 963, persistent)
+ * QZ_PAIR_WT, QZ_PAIR_PS, QZ_PAIR_WK1, and QZ_GEMM16_SCHED -- the schedule qz_gemm_16bit (default 971, persistent)
  * launches: environment variables read ONCE when the library is loaded) and the
  * device's CU count, as a JSON object written to buf (NUL-terminated when n > the length).
  * Returns the length of the JSON text.  No reference counterpart (measurement bookkeeping). */

@@ -1952,7 +1952,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const f4_t lo = acc[2 * J][i], hi = acc[2 * J + 1][i];
         const v4u o = v4u{cvt_pk16<DT>(lo[0] + bv[0], lo[1] + bv[1]), cvt_pk16<DT>(lo[2] + bv[2], lo[3] + bv[3]),
                           cvt_pk16<DT>(hi[0] + bv[4], hi[1] + bv[5]), cvt_pk16<DT>(hi[2] + bv[6], hi[3] + bv[7])};
-        if (t < p.T && m < p.M) *reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m) = o;
+        if (t < p.T && m < p.M) {
+          v4u *dst = reinterpret_cast<v4u *>(reinterpret_cast<uint16_t *>(p.Y) + (size_t)t * p.ldy + m);
+          if constexpr ((S & 8) != 0) __builtin_nontemporal_store(o, dst);   // S & 8: streaming stores
+          else *dst = o;
+        }
       }
     }
     if (!more) break;
@@ -2367,7 +2371,10 @@ static bool mt_ok(int T, int K) { return T >= 2 && T <= 16 && K % kMtChunk == 0;
 // the waves on odd SIMDs run the schedule one MFMA later, 64 (with 1) each step one hand-ordered asm
 // stream (gemm16_asm_step.h), 128 (with 64) the library's two event orders by SIMD parity, 512 (with
 // 64 | 2) the persistent k_gemm16_4q where K / 64 is even, 256 (with 512) W's k-half 1 fragments
-// read and its image refilled before X's.  Default 963 = 512 | 256 | 128 | 64 | 2 | 1
+// read and its image refilled before X's, 8 (with 512 | 256) the epilogue's stores non-temporal where
+// K <= 8192 (the output is not re-read by this launch; it stops evicting the X / W k-slices that other
+// tiles re-read).
+// Default 971 = 512 | 256 | 128 | 64 | 8 | 2 | 1
 namespace qz {
 int &gemm16_sched();  // gemv.hip: QZ_GEMM16_SCHED
 }
@@ -2401,13 +2408,18 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
   // buffer 0 (K / 64 even); otherwise the schedule's non-persistent kernel
   if ((sched & 512) != 0 && (K / kBK) % 2 == 0) {
     const unsigned gq = std::min(g, (unsigned)device_cus());
+    // bit 8: non-temporal output stores where the output is large against the K loop (K <= 8192:
+    // measured faster at K = 4096, slower at 14336 -- profiles/r6_gemm16_nt_store_sweeps.txt)
+    const bool nt_out = K <= 8192;
 #define QZ_G16Q(DT_, S_) hipLaunchKernelGGL((k_gemm16_4q<DT_, S_>), dim3(gq), dim3(256), 0, s, p)
     if (dtype == QZ_DT_F16) {
-      if (sched & 256) QZ_G16Q(QZ_DT_F16, 384);
+      if ((sched & 264) == 264 && nt_out) QZ_G16Q(QZ_DT_F16, 392);
+      else if (sched & 256) QZ_G16Q(QZ_DT_F16, 384);
       else if (sched & 128) QZ_G16Q(QZ_DT_F16, 128);
       else QZ_G16Q(QZ_DT_F16, 0);
     } else {
-      if (sched & 256) QZ_G16Q(QZ_DT_BF16, 384);
+      if ((sched & 264) == 264 && nt_out) QZ_G16Q(QZ_DT_BF16, 392);
+      else if (sched & 256) QZ_G16Q(QZ_DT_BF16, 384);
       else if (sched & 128) QZ_G16Q(QZ_DT_BF16, 128);
       else QZ_G16Q(QZ_DT_BF16, 0);
     }
@@ -2415,9 +2427,11 @@ extern "C" int qz_gemm_16bit(int T, int M, int K, const void *X, int ldx, int dt
     QZ_LAUNCH_CHECK();
     return QZ_OK;
   }
+  // the non-persistent schedule (bit 8 of a persistent schedule is its store policy, not 4d's rotation)
+  const int s4d = (sched & 512) ? (sched & 255 & ~8) : (sched & 255);
 #define QZ_G16(DT_, S_) hipLaunchKernelGGL((k_gemm16_4d<DT_, 64, 16, 112, S_>), dim3(g), dim3(256), 0, s, p)
 #define QZ_G16S(DT_)                   \
-  switch (sched & 255) {               \
+  switch (s4d) {                       \
     case 1: QZ_G16(DT_, 1); break;     \
     case 2: QZ_G16(DT_, 2); break;     \
     case 3: QZ_G16(DT_, 3); break;     \

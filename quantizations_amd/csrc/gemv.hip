@@ -61,10 +61,10 @@ static Knobs read_knobs() {
 }
 static Knobs g_knobs = read_knobs();   // at library load
 Knobs &gemv_knobs() { return g_knobs; }
-// QZ_GEMM16_SCHED: the k_gemm16_4d / k_gemm16_4q schedule qz_gemm_16bit launches (gemm.hip); 963 =
+// QZ_GEMM16_SCHED: the k_gemm16_4d / k_gemm16_4q schedule qz_gemm_16bit launches (gemm.hip); 971 =
 // the persistent asm-step form with the library's dual event order, W's fragments read and refilled
-// first: the fastest measured (all bit-identical)
-static int g_gemm16_sched = env_int("QZ_GEMM16_SCHED", 963);
+// first, non-temporal output stores: the fastest measured (all bit-identical)
+static int g_gemm16_sched = env_int("QZ_GEMM16_SCHED", 971);
 int &gemm16_sched() { return g_gemm16_sched; }
 
 template <bool DQ, int DT, int R, int WK, int NW, bool FS, bool CL, bool WT, bool TWO, int STAMP = 0>

@@ -69,5 +69,5 @@ for (M, K, T) in [(4096, 4096, 16384), (14336, 4096, 16384), (4096, 14336, 16384
     out[f"{M}x{K} T={T}"] = res
     print(f"{M}x{K} T={T}", json.dumps(res), flush=True)
     del x, W
-_lib.set_gemv_knob("QZ_GEMM16_SCHED", 963)
+_lib.set_gemv_knob("QZ_GEMM16_SCHED", 971)
 print(json.dumps(out))

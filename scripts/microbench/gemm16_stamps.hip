@@ -5,7 +5,7 @@
 #define QZ_STAMPS_G16
 #endif
 #include "../../quantizations_amd/csrc/gemm.hip"
-namespace qz { int &gemm16_sched() { static int v = 963; return v; } }  // the library keeps it in gemv.hip
+namespace qz { int &gemm16_sched() { static int v = 971; return v; } }  // the library keeps it in gemv.hip
 
 #include <algorithm>
 #include <cstdio>
@@ -42,7 +42,7 @@ int main(int argc, char **argv) {
   std::vector<V> vs;
 #define ADD(SK_, S_) vs.push_back({"SK=" #SK_ " S=" #S_, [=]() { hipLaunchKernelGGL((k_gemm16_4d<QZ_DT_F16, SK_, 16, 112, S_>), dim3(g), dim3(256), 0, 0, p); }, {}, {}})
 #define ADDQ(S_) vs.push_back({"4q S=" #S_, [=]() { hipLaunchKernelGGL((k_gemm16_4q<QZ_DT_F16, S_>), dim3(std::min(g, 256u)), dim3(256), 0, 0, p); }, {}, {}})
-  ADD(64, 0); ADD(65, 0); ADDQ(0); ADDQ(128); ADDQ(384);
+  ADD(64, 0); ADD(65, 0); ADDQ(0); ADDQ(128); ADDQ(384); ADDQ(392);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto &v : vs) v.f();
   CK(hipDeviceSynchronize());

@@ -1,4 +1,4 @@
-"""qz_gemm_16bit (schedule QZ_GEMM16_SCHED, default 963) and hipBLASLt (F.linear) on the same randn fp16
+"""qz_gemm_16bit (schedule QZ_GEMM16_SCHED, default 971) and hipBLASLt (F.linear) on the same randn fp16
 operands, for rocprofv3 passes: config #4's 4096 x 4096 at T = 16384 unless M K T are given.
    python scripts/prof_gemm16.py [iters] [M K T]"""
 import os

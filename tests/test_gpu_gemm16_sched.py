@@ -12,15 +12,15 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 # 512 |: the persistent k_gemm16_4q (one workgroup per CU, the next tile's steps 0 / 1 staged by the
 # last two steps of a tile) where K / 64 is even, else the non-persistent schedule; 963 = 707 | 256:
-# W's k-half 1 fragments read (and its image refilled) before X's
-SCHEDS = [1, 2, 3, 9, 11, 25, 27, 65, 67, 193, 195, 579, 707, 963]
+# W's k-half 1 fragments read (and its image refilled) before X's; 971 = 963 | 8: non-temporal stores
+SCHEDS = [1, 2, 3, 9, 11, 25, 27, 65, 67, 193, 195, 579, 707, 963, 971]
 
 
 @pytest.fixture
 def sched_knob():
     from quantizations_amd import _lib
 
-    before = _lib.gemv_knobs().get("QZ_GEMM16_SCHED", 963)
+    before = _lib.gemv_knobs().get("QZ_GEMM16_SCHED", 971)
     yield lambda s: _lib.set_gemv_knob("QZ_GEMM16_SCHED", s)
     _lib.set_gemv_knob("QZ_GEMM16_SCHED", before)
 

@@ -51,3 +51,24 @@ def test_gemm16_schedules_bit_identical(sched_knob, T, M, K, dtype, bias):
         torch.cuda.synchronize()
         ndiff = int((y != ref).sum().item())
         assert ndiff == 0, f"schedule {s}: {ndiff} of {y.numel()} outputs differ from schedule 0"
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("T,M,K", [(4096, 1024, 4096), (300, 264, 256), (8192, 4096, 128)])
+def test_gemm16_strided_activation_rows(sched_knob, T, M, K, dtype):
+    """X as a column slice of a wider tensor (row stride K + 64, the C-ABI's ldx > K): the DMA
+    offsets of the default persistent schedule and of schedule 0 give the same bits as on the
+    contiguous copy."""
+    from quantizations_amd.core import gemm_16bit
+
+    g = torch.Generator(device="cuda").manual_seed(T + M + K)
+    W = (torch.randn(M, K, device=DEV, generator=g) * 0.02).to(dtype)
+    Xw = torch.randn(T, K + 64, device=DEV, generator=g).to(dtype)
+    X = Xw[:, :K]
+    assert X.stride(0) == K + 64
+    for s in (0, 971):
+        sched_knob(s)
+        y_strided = gemm_16bit(X, W)
+        y_contig = gemm_16bit(X.contiguous(), W)
+        torch.cuda.synchronize()
+        assert torch.equal(y_strided, y_contig), f"schedule {s}"
